@@ -1,0 +1,99 @@
+"""Airframe / task configuration: our parameter file -> `hg_config` (include/heligym_amd.h).
+
+Mirrors what the reference does in Heli.__init__ (heligym/envs/helicopter.py:47-62: yaml load,
+DT, default max time / target / trim condition) and the task constructors
+(heligym/envs/helicopter_with_tasks.py:6-25, 56-76).
+"""
+import copy
+import os
+
+import numpy as np
+import yaml
+
+from . import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+FPS = 50.0
+DT = 1.0 / FPS                       # helicopter.py:18-19
+DEFAULT_MAX_TIME = 40.0              # helicopter.py:33-34
+DEFAULT_TRIM_COND = {                # helicopter.py:36-44
+    "yaw": 0.0, "yaw_rate": 0.0, "ned_vel": [0.0, 0.0, 0.0], "gr_alt": 100.0,
+    "xy": [0.0, 0.0], "psi_mr": 0.0, "psi_tr": 0.0,
+}
+TASKS = {"heli": _abi.HG_TASK_HELI, "hover": _abi.HG_TASK_HOVER,
+         "forward_flight": _abi.HG_TASK_FORWARD_FLIGHT}
+# Task targets: helicopter_with_tasks.py:9-13 (hover) and :59-63 (forward flight).
+DEFAULT_TARGETS = {
+    "heli": {},
+    "hover": {"sea_alt": 4000.0, "north_loc": 0.0, "east_loc": 0.0},
+    "forward_flight": {"sea_alt": 4000.0, "heading": 0.0, "vel": 100.0},
+}
+TARGET_KEYS = ("north_loc", "east_loc", "sea_alt", "heading", "vel")
+
+
+def load_airframe(heli_name="aw109"):
+    path = os.path.join(_HERE, "helis", heli_name + ".yaml")
+    with open(path) as f:
+        doc = yaml.safe_load(f)
+    return doc
+
+
+def load_terrain(doc):
+    """uint16 [rows, cols] samples and their scale to ft (helicopter_dynamics.py:39-43)."""
+    path = os.path.join(_HERE, doc["terrain"]["file"])
+    with np.load(path, allow_pickle=False) as z:
+        u16 = np.ascontiguousarray(z["hmap"], dtype=np.uint16)
+    return u16
+
+
+def terrain_ft(u16, max_gr_alt):
+    """Heights in ft as float32 (the kernel's table); reference: png / 65535 * MAX_GR_ALT."""
+    return ((u16.astype(np.float64) / 65535.0) * max_gr_alt).astype(np.float32)
+
+
+def fill_trim(tc, trim_cond):
+    d = copy.deepcopy(DEFAULT_TRIM_COND)
+    d.update(trim_cond or {})
+    tc.yaw, tc.yaw_rate = float(d["yaw"]), float(d["yaw_rate"])
+    for i in range(3):
+        tc.ned_vel[i] = float(d["ned_vel"][i])
+    tc.gr_alt = float(d["gr_alt"])
+    tc.xy[0], tc.xy[1] = float(d["xy"][0]), float(d["xy"][1])
+    tc.psi_mr, tc.psi_tr = float(d["psi_mr"]), float(d["psi_tr"])
+    return d
+
+
+def fill_target(tg, target):
+    t = dict.fromkeys(TARGET_KEYS, 0.0)
+    t.update(target or {})
+    for k in TARGET_KEYS:
+        setattr(tg, k, float(t[k]))
+    return t
+
+
+def make_config(task="hover", dt=DT, heli_name="aw109", max_time=None, target=None,
+                trim_cond=None, autoreset=True, seed=0, env_offset=0, turbulence_level=None):
+    doc = load_airframe(heli_name)
+    cfg = _abi.hg_config()
+    af = doc["airframe"]
+    for name, _ in _abi.hg_airframe._fields_:
+        if name == "_pad0":
+            continue
+        if name == "env_TURB_LVL":
+            cfg.af.env_TURB_LVL = int(af[name] if turbulence_level is None else turbulence_level)
+        else:
+            setattr(cfg.af, name, float(af[name]))
+    if task not in TASKS:
+        raise ValueError(f"unknown task {task!r}; one of {sorted(TASKS)}")
+    fill_trim(cfg.trim, trim_cond)
+    tgt = dict(DEFAULT_TARGETS[task])
+    tgt.update(target or {})
+    fill_target(cfg.target, tgt)
+    cfg.dt = float(dt)
+    cfg.max_time = float(DEFAULT_MAX_TIME if max_time is None else max_time)
+    cfg.task = TASKS[task]
+    cfg.autoreset = 1 if autoreset else 0
+    cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    cfg.env_offset = int(env_offset)
+    return cfg, doc

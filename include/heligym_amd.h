@@ -1,0 +1,191 @@
+/*
+ * heligym_amd.h — C-ABI of the MI355X-native vectorised heli-gym step().
+ *
+ * The reference (ugurcanozalp/heli-gym v2) has no FFI on this path: its boundary is the
+ * gymnasium `Heli` env (heligym/envs/helicopter.py:28-243) calling two Python
+ * `DynamicSystem.step` objects (heligym/envs/dynamics/dynamics.py:158-171).  Each entry point
+ * below replaces one piece of that surface; the reference file:line it replaces is cited on it.
+ * The only native precedent in the reference is its renderer C-ABI
+ * (heligym/envs/renderer/src/py_api.h:17-90, opaque handles, ctypes-bound in pyapi.py:9-32);
+ * this header follows the same opaque-handle style but every call returns an error code.
+ *
+ * Conventions
+ *  - Units are the reference's US customary units (ft, slug, lb, s, rad).
+ *  - All `*_dev` pointers are device (HBM) pointers owned by the caller, e.g. PyTorch-ROCm
+ *    tensors; `stream` is a hipStream_t passed as void* (NULL = default stream).  Device calls
+ *    are asynchronous on `stream`, never synchronise, never allocate, and are hipGraph-capturable.
+ *  - Host pointers are plain host memory.  Sizes are element counts.
+ *  - Return value: HG_OK (0) or a negative HG_E_* code; hg_last_error() gives the message of the
+ *    last failure on the calling thread.  A handle is not re-entrant: one stream/thread at a time.
+ *  - Layouts: actions [N,4] fp32 row-major; obs [N,17] fp32 row-major in the reference order
+ *    (helicopter_dynamics.py:23-25); per-env state record [N,HG_STATE_COLS] fp32 (see below).
+ */
+#ifndef HELIGYM_AMD_H
+#define HELIGYM_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HG_ABI_VERSION 1
+
+#define HG_N_OBS 17        /* helicopter_dynamics.py:23-27 */
+#define HG_N_ACT 4         /* helicopter_dynamics.py:28 */
+#define HG_N_HELI 18       /* vi_mr vi_tr psi_mr psi_tr betas[2] uvw[3] pqr[3] euler[3] xyz[3] (:55-64) */
+#define HG_N_WIND 5        /* us vs[2] ws[2] (wind_dynamics.py:39-42) */
+#define HG_N_CARRY 4       /* previous obs N_VEL, E_VEL, DES_RATE, GROUND_ALTITUDE (helicopter.py:195-196) */
+/* state record columns: heli[18] | wind[5] | carry[4] */
+#define HG_STATE_COLS (HG_N_HELI + HG_N_WIND + HG_N_CARRY)
+/* counter record columns (int32): episode step, success steps, episode index */
+#define HG_COUNTER_COLS 3
+
+enum {
+    HG_OK = 0,
+    HG_E_INVALID = -1,   /* bad argument / shape */
+    HG_E_HIP = -2,       /* HIP runtime error (no device, launch failure, ...) */
+    HG_E_TRIM = -3,      /* trim did not converge (helicopter_dynamics.py:543-544) */
+    HG_E_NOMEM = -4
+};
+
+/* Tasks: helicopter.py:242-243 (Heli, reward 0), helicopter_with_tasks.py:5-52 (HeliHover),
+ * helicopter_with_tasks.py:54-115 (HeliForwardFlight). */
+enum { HG_TASK_HELI = 0, HG_TASK_HOVER = 1, HG_TASK_FORWARD_FLIGHT = 2 };
+
+/* info bit-field written per env by hg_step (helicopter.py:219-224). */
+enum { HG_INFO_FAILED = 1, HG_INFO_SUCCESSED = 2, HG_INFO_TIME_UP = 4, HG_INFO_SUCCESS_STEP = 8 };
+
+/* Raw airframe + environment parameters: the fields of heligym/envs/helis/aw109.yaml:2-101. */
+typedef struct hg_airframe {
+    /* ENV (aw109.yaml:2-16) */
+    double env_R, env_T0, env_LAPSE, env_RO_SEA, env_GRAV, env_MAX_GR_ALT, env_NS_MAX, env_EW_MAX;
+    double env_WIND_DIR_deg, env_WIND_SPD;
+    int32_t env_TURB_LVL, _pad0;
+    /* HELI (aw109.yaml:18-37) */
+    double HP_LOSS, VTRANS, FS_CG, WL_CG, WT, IX, IY, IZ, IXZ;
+    double COL_OS, COL_L, COL_H, LON_L, LON_H, LAT_L, LAT_H, PED_OS, PED_L, PED_H;
+    /* MR (:39-52) */
+    double mr_FS, mr_WL, mr_IS, mr_E, mr_IB, mr_R, mr_A, mr_RPM, mr_CD0, mr_B, mr_C, mr_TWST, mr_K1;
+    /* TR (:54-63) */
+    double tr_FS, tr_WL, tr_R, tr_A, tr_C, tr_RPM, tr_CD0, tr_TWST, tr_B;
+    /* FUS (:65-71) */
+    double fus_FS, fus_WL, fus_XUU, fus_YVV, fus_ZWW, fus_COR;
+    /* HT (:73-78) */
+    double ht_FS, ht_WL, ht_ZUU, ht_ZUW, ht_ZMAX;
+    /* VT (:80-85) */
+    double vt_FS, vt_WL, vt_YUU, vt_YUV, vt_YMAX;
+    /* WN (:87-93) */
+    double wn_FS, wn_WL, wn_ZUU, wn_ZUW, wn_ZMAX, wn_B;
+    /* LG (:95-101) */
+    double lg_K, lg_C, lg_BL_MN, lg_FS_MN, lg_FS_N, lg_WL;
+} hg_airframe;
+
+/* Trim condition (helicopter.py:36-44, helicopter_dynamics.py:45-53, consumed by trim :491-555). */
+typedef struct hg_trim_cond {
+    double yaw, yaw_rate, ned_vel[3], gr_alt, xy[2], psi_mr, psi_tr;
+} hg_trim_cond;
+
+/* Task target (helicopter_with_tasks.py:9-13, 59-63): north_loc, east_loc, sea_alt, heading, vel. */
+typedef struct hg_target {
+    double north_loc, east_loc, sea_alt, heading, vel;
+} hg_target;
+
+typedef struct hg_config {
+    hg_airframe af;
+    hg_trim_cond trim;
+    hg_target target;
+    double dt;            /* helicopter.py:18-19 (1/FPS = 0.02); north star uses 0.01 */
+    double max_time;      /* helicopter.py:33-34,89-92 (40 s) */
+    int32_t task;         /* HG_TASK_* */
+    int32_t autoreset;    /* 1: reset finished envs inside hg_step (same-step autoreset) */
+    uint64_t seed;        /* Philox key for the turbulence noise (wind_dynamics.py:49-52) */
+    int64_t env_offset;   /* global id of local env 0 (sharding: results independent of rank count) */
+} hg_config;
+
+/* Reset template produced by the trim (host values). */
+typedef struct hg_trim_result {
+    double state[HG_N_HELI];       /* trimmed heli state (fp32-rounded, as the reference stores it) */
+    double action[HG_N_ACT];       /* trim controls */
+    double obs[HG_N_OBS];          /* observation at the trim state */
+    double state_dots[HG_N_HELI];  /* dynamics at the trim state */
+    double residual;               /* final ||y - y*||^2 of the Newton iteration */
+    int32_t iterations;
+    int32_t failed;                /* reset-time _is_failed() (helicopter.py:226-234) */
+} hg_trim_result;
+
+typedef struct hg_env hg_env;
+
+/* Library / error ----------------------------------------------------------------------------- */
+int32_t hg_abi_version(void);
+const char* hg_last_error(void);
+
+/* Fill `cfg` with the AW109 / HeliHover defaults (aw109.yaml, helicopter.py:18-44,
+ * helicopter_with_tasks.py:5-25).  Host only. */
+void hg_default_config(hg_config* cfg);
+
+/* Trim (host, fp64).  Replaces HelicopterDynamics.trim / __trim_fcn
+ * (helicopter_dynamics.py:491-576) as called from reset (:66-71).  `terrain_ft` is the
+ * [rows, cols] ground-height map in ft (helicopter_dynamics.py:39-43), `wind_ned` the wind the
+ * trim is solved against (helicopter.py:55: the mean wind). */
+int32_t hg_trim(const hg_config* cfg, const float* terrain_ft, int32_t rows, int32_t cols,
+                const double wind_ned[3], hg_trim_result* out);
+
+/* Handle lifetime: replaces Heli.__init__ (helicopter.py:47-86: yaml params, HelicopterDynamics
+ * and WindDynamics construction, terrain load) for `num_envs` independent helicopters, and
+ * Heli.close (helicopter.py:185-187).  Uploads the terrain, derives the model constants, trims
+ * the reset template against the mean wind. */
+int32_t hg_create(const hg_config* cfg, const float* terrain_ft, int32_t rows, int32_t cols,
+                  int64_t num_envs, hg_env** out);
+void hg_destroy(hg_env* env);
+int64_t hg_num_envs(const hg_env* env);
+
+/* Setters: Heli.set_max_time (helicopter.py:89-92), set_target (:94-96), set_trim_cond
+ * (:101-103; re-trims the reset template).  Host only; affect subsequent device calls. */
+int32_t hg_set_max_time(hg_env* env, double max_time);
+int32_t hg_set_target(hg_env* env, const hg_target* target);
+int32_t hg_set_trim_cond(hg_env* env, const hg_trim_cond* trim);
+int32_t hg_get_template(const hg_env* env, hg_trim_result* out);
+
+/* Reset: replaces Heli.reset (helicopter.py:208-217) -> WindDynamics.reset (wind_dynamics.py:44-47)
+ * + HelicopterDynamics.reset (helicopter_dynamics.py:66-71).  Envs with mask_dev[i] != 0 (all
+ * envs if mask_dev == NULL) get the trimmed state, zero turbulence state, zero counters; their
+ * observation row is written to obs_dev [N,17] (other rows untouched). */
+int32_t hg_reset(hg_env* env, const uint8_t* mask_dev, float* obs_dev, void* stream);
+
+/* Step: replaces Heli.step (helicopter.py:192-206) with everything it calls — WindDynamics.step
+ * (dynamics.py:158-171 + wind_dynamics.py:49-125), HelicopterDynamics.step (dynamics.py:158-171
+ * + helicopter_dynamics.py:73-77,400-489), the task reward (helicopter_with_tasks.py:27-52 /
+ * 78-115) and _get_info (helicopter.py:219-240) — for all N envs in one kernel launch.
+ *   actions_dev     [N,4]  fp32 in (no clipping, like the reference)
+ *   obs_dev         [N,17] fp32 out (for auto-reset envs: the reset observation)
+ *   reward_dev      [N]    fp32 out
+ *   terminated_dev  [N]    u8 out   (failed or successed; helicopter.py:203)
+ *   truncated_dev   [N]    u8 out   (time_up; helicopter.py:204)
+ *   info_dev        [N]    u8 out or NULL (HG_INFO_* bits)
+ *   eta_dev         [N,3]  fp32 in or NULL: turbulence noise already scaled by 1/sqrt(dt)
+ *                          (parity / replay); NULL = in-kernel Philox4x32-10 normals keyed by
+ *                          (seed, env_offset+i, episode, step)
+ *   reset_count_dev [1]    i32 out or NULL: number of envs auto-reset this step (zeroed here)
+ *   reset_index_dev [N]    i32 out or NULL: compacted ids of those envs (wave-ballot order)
+ *   final_obs_dev   [N,17] fp32 out or NULL: their terminal observations, same compacted order */
+int32_t hg_step(hg_env* env, const float* actions_dev, float* obs_dev, float* reward_dev,
+                uint8_t* terminated_dev, uint8_t* truncated_dev, uint8_t* info_dev,
+                const float* eta_dev, int32_t* reset_count_dev, int32_t* reset_index_dev,
+                float* final_obs_dev, void* stream);
+
+/* State access for parity tests / checkpointing (the reference's StateNumpy,
+ * dynamics.py:75-128, exposed as one record per env): state [N,HG_STATE_COLS] fp32,
+ * counters [N,HG_COUNTER_COLS] i32 (either may be NULL). */
+int32_t hg_get_state(hg_env* env, float* state_dev, int32_t* counters_dev, void* stream);
+int32_t hg_set_state(hg_env* env, const float* state_dev, const int32_t* counters_dev, void* stream);
+
+/* Synthetic policy for benchmarks: actions [N,4] ~ U(lo, hi) from Philox4x32-10 keyed by
+ * (seed, env_offset+i, step).  Not part of the reference surface. */
+int32_t hg_random_actions(hg_env* env, float* actions_dev, uint64_t seed, uint64_t step,
+                          float lo, float hi, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HELIGYM_AMD_H */

@@ -1,0 +1,157 @@
+"""ctypes wrapper of oracle/liboracle.so (the C restatement in heli_oracle.c).
+
+TEST INFRASTRUCTURE ONLY — imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg; never by the product package.  Builds on demand with gcc.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+SRC = os.path.join(HERE, "heli_oracle.c")
+
+
+def build(force=False):
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
+        subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",
+                               "-Wno-unused-function", "-o", LIB, SRC, "-lm"])
+    return LIB
+
+
+class or_env(ctypes.Structure):
+    _fields_ = [("heli", ctypes.c_double * 18), ("wind", ctypes.c_double * 5),
+                ("obs", ctypes.c_double * 17), ("dots", ctypes.c_double * 18),
+                ("time_counter", ctypes.c_double), ("successed_time", ctypes.c_double),
+                ("state_f32", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+
+
+class or_out(ctypes.Structure):
+    _fields_ = [("obs", ctypes.c_double * 17), ("wind_ned", ctypes.c_double * 3),
+                ("reward_hover", ctypes.c_double), ("reward_ff", ctypes.c_double),
+                ("reward", ctypes.c_double)] + [
+        (n, ctypes.c_int32) for n in ("success_hover", "success_ff", "failed", "successed",
+                                      "time_up", "terminated", "truncated", "_pad")]
+
+
+def _dp(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+class Oracle:
+    def __init__(self, cfg, hmap_u16):
+        from heligym_amd import _abi
+        self._abi = _abi
+        lib = ctypes.CDLL(build())
+        self.lib = lib
+        D = ctypes.c_double
+        PD = ctypes.POINTER(D)
+        lib.or_create.restype = ctypes.c_void_p
+        lib.or_create.argtypes = [ctypes.POINTER(_abi.hg_config), ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        lib.or_free.argtypes = [ctypes.c_void_p]
+        lib.or_const.restype = D
+        lib.or_const.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        lib.or_lg_loc.argtypes = [ctypes.c_void_p, PD]
+        lib.or_pi_bound.restype = D
+        lib.or_pi_bound.argtypes = [D]
+        lib.or_lut2d.restype = D
+        lib.or_lut2d.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int, D, D]
+        lib.or_ground_height_p.restype = D
+        lib.or_ground_height_p.argtypes = [ctypes.c_void_p, D, D, ctypes.c_int]
+        lib.or_lut2d_f64.restype = D
+        lib.or_lut2d_f64.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.c_int, D, D]
+        lib.or_dryden_params.argtypes = [ctypes.c_void_p, D, PD, PD]
+        lib.or_wind_step.argtypes = [ctypes.c_void_p, PD, PD, PD, PD]
+        lib.or_dynamics.argtypes = [ctypes.c_void_p, PD, PD, PD, D, PD, PD]
+        lib.or_heli_step.argtypes = [ctypes.c_void_p, PD, PD, PD, PD, PD, ctypes.c_int]
+        lib.or_is_failed.restype = ctypes.c_int
+        lib.or_is_failed.argtypes = [ctypes.c_void_p, PD, PD]
+        lib.or_step.argtypes = [ctypes.c_void_p, ctypes.POINTER(or_env), PD, PD, ctypes.POINTER(or_out)]
+        lib.or_trim.restype = ctypes.c_int
+        lib.or_trim.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.hg_trim_cond), PD,
+                                ctypes.POINTER(_abi.hg_trim_result)]
+        lib.or_reset.argtypes = [ctypes.c_void_p, ctypes.POINTER(or_env), ctypes.POINTER(_abi.hg_trim_result)]
+        lib.or_rollout.restype = ctypes.c_int64
+        lib.or_rollout.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.hg_trim_result), ctypes.c_int64,
+                                   ctypes.c_int64, ctypes.c_uint64, PD]
+        self.cfg = cfg
+        self._hmap = np.ascontiguousarray(hmap_u16, dtype=np.uint16)
+        self.m = lib.or_create(ctypes.byref(cfg), self._hmap.ctypes.data, self._hmap.shape[0],
+                               self._hmap.shape[1])
+
+    def __del__(self):
+        try:
+            self.lib.or_free(self.m)
+        except Exception:
+            pass
+
+    # --- KAT-level functions
+    def const(self, name):
+        return self.lib.or_const(self.m, name.encode())
+
+    def lg_loc(self):
+        o = np.zeros(9)
+        self.lib.or_lg_loc(self.m, _dp(o))
+        return o.reshape(3, 3)
+
+    def pi_bound(self, x):
+        return self.lib.or_pi_bound(float(x))
+
+    def lut2d(self, table, rk, ck, f64=False):
+        t = np.ascontiguousarray(table, dtype=np.float32)
+        fn = self.lib.or_lut2d_f64 if f64 else self.lib.or_lut2d
+        return fn(t.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), t.shape[0] - 1, t.shape[1] - 1,
+                  float(rk), float(ck))
+
+    def ground_height(self, x, y, state_f32=False):
+        return self.lib.or_ground_height_p(self.m, float(x), float(y), int(bool(state_f32)))
+
+    def dryden(self, h, vel_inf):
+        v = np.ascontiguousarray(vel_inf, dtype=np.float64)
+        o = np.zeros(7)
+        self.lib.or_dryden_params(self.m, float(h), _dp(v), _dp(o))
+        return o
+
+    def trim(self, trim_cond=None, wind=None):
+        from heligym_amd import config
+        tc = self._abi.hg_trim_cond()
+        config.fill_trim(tc, trim_cond or {})
+        w = np.ascontiguousarray(wind if wind is not None else [self.const("WIND_N"), self.const("WIND_E"), 0.0],
+                                 dtype=np.float64)
+        r = self._abi.hg_trim_result()
+        rc = self.lib.or_trim(self.m, ctypes.byref(tc), _dp(w), ctypes.byref(r))
+        if rc != 0:
+            raise RuntimeError("oracle trim failed")
+        return r
+
+    # --- env level
+    def env_from(self, heli, wind, obs, dots, time_counter=0.0, successed_time=0.0, state_f32=False):
+        e = or_env()
+        e.heli[:] = list(map(float, heli))
+        e.wind[:] = list(map(float, wind))
+        e.obs[:] = list(map(float, obs))
+        e.dots[:] = list(map(float, dots))
+        e.time_counter = float(time_counter)
+        e.successed_time = float(successed_time)
+        e.state_f32 = int(bool(state_f32))
+        return e
+
+    def env_reset(self, tr):
+        e = or_env()
+        self.lib.or_reset(self.m, ctypes.byref(e), ctypes.byref(tr))
+        return e
+
+    def step(self, e, action, eta):
+        a = np.ascontiguousarray(action, dtype=np.float64)
+        n = np.ascontiguousarray(eta, dtype=np.float64)
+        o = or_out()
+        self.lib.or_step(self.m, ctypes.byref(e), _dp(a), _dp(n), ctypes.byref(o))
+        return o
+
+    def rollout(self, tr, n_envs, n_steps, seed=0):
+        cs = ctypes.c_double()
+        n = self.lib.or_rollout(self.m, ctypes.byref(tr), int(n_envs), int(n_steps), int(seed),
+                                ctypes.byref(cs))
+        return n, cs.value

@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ from the reference (this container only).
+
+Runs the unmodified reference Python path (loaded by `tools/refload.py`) and stores
+inputs and outputs as small `.npz` data files (no pickles).  Nothing under
+`/root/reference` is copied: only numbers the reference computed.
+
+Fixtures
+--------
+kats.npz         known-answer values: derived AW109 constants
+                 (helicopter_dynamics.py:107-154), LookUpTable KATs (lookup.py:43-65,192-202),
+                 Dryden `_calc_params` (wind_dynamics.py:54-83), terrain height lookups
+                 (helicopter_dynamics.py:167-195), pi_bound (utils.py:3-4).
+trim.npz         Newton trim results (helicopter_dynamics.py:491-576) for several trim
+                 conditions at dt 0.02 and 0.01, and the 2nd-episode reset (F8).
+traj_dt0.02.npz  per-step trajectories of `Heli.step` (helicopter.py:192-206) for
+traj_dt0.01.npz  scenarios covering every branch of the step (see SCENARIOS), with the
+                 recorded turbulence noise `eta` so the step can be replayed exactly.
+
+Usage: python tools/gen_goldens.py   (numpy 2.2.6 promotion rules are part of the result)
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import refload  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
+
+DEFAULT_TRIM = {"yaw": 0.0, "yaw_rate": 0.0, "ned_vel": [0.0, 0.0, 0.0], "gr_alt": 100.0,
+                "xy": [0.0, 0.0], "psi_mr": 0.0, "psi_tr": 0.0}
+
+# name -> (trim overrides, action kind, max steps)
+SCENARIOS = [
+    ("hover_zero", {}, "zero", 700),
+    ("hover_random", {}, "uniform", 700),
+    ("hover_trimnoise", {}, "trim_noise", 400),
+    ("alt1500_medium", {"gr_alt": 1500.0}, "trim_noise", 300),
+    ("alt2500_high", {"gr_alt": 2500.0}, "trim_noise", 300),
+    ("forward80", {"ned_vel": [80.0, 0.0, 0.0]}, "trim_noise", 300),
+    ("edge_exit", {"xy": [3150.0, -3150.0], "ned_vel": [60.0, -60.0, 0.0]}, "trim", 400),
+    ("crash_lowcoll", {}, "low_collective", 600),
+    ("yawrate", {"yaw_rate": 0.1, "yaw": 1.0, "psi_mr": 0.3, "psi_tr": -0.2}, "trim_noise", 300),
+    # ~4000 ft above sea level = the tasks' target altitude: success steps accumulate and the
+    # episode ends by `successed` (helicopter.py:236-237) after max_time/4 of success.
+    ("hover_at_target", {"gr_alt": 2453.3}, "trim", 700),
+    ("forward100_target", {"gr_alt": 2453.3, "ned_vel": [100.0, 0.0, 0.0]}, "trim", 300),
+]
+
+TRIM_CASES = [
+    {},
+    {"gr_alt": 1500.0},
+    {"gr_alt": 2500.0},
+    {"ned_vel": [80.0, 0.0, 0.0]},
+    {"ned_vel": [30.0, 20.0, -5.0]},
+    {"yaw_rate": 0.1, "yaw": 1.0},
+    {"xy": [3150.0, -3150.0], "ned_vel": [60.0, -60.0, 0.0]},
+    {"xy": [-1000.0, 2000.0], "gr_alt": 50.0},
+]
+
+
+def trim_vec(c):
+    d = dict(DEFAULT_TRIM)
+    d.update(c)
+    return np.array([d["yaw"], d["yaw_rate"], *d["ned_vel"], d["gr_alt"], *d["xy"],
+                     d["psi_mr"], d["psi_tr"]], dtype=np.float64)
+
+
+def make_env(ns, dt):
+    ns.helicopter.DT = dt  # module constant read by Heli.__init__/step (helicopter.py:18-19,53-54,193,205)
+    env = ns.tasks.HeliHover()
+    env.set_target({"vel": 100, "heading": 0})  # keys ForwardFlight's reward reads (shared dict)
+    return env
+
+
+def ff_reward(ns, env):
+    return ns.tasks.HeliForwardFlight._calculate_reward(env)
+
+
+def gen_kats(ns):
+    out = {}
+    env = make_env(ns, 0.02)
+    hd = env.heli_dyn
+    names, vals = [], []
+    for comp, keys in [("MR", ["H", "D", "OMEGA", "V_TIP", "FR", "SOL", "A_SIGMA", "GAM_OM16_DRO",
+                               "DL_DB1", "DL_DA1_DRO", "COEF_TH"]),
+                       ("TR", ["H", "D", "OMEGA", "V_TIP", "FR", "SOL", "COEF_TH"]),
+                       ("FUS", ["H", "D"]), ("HT", ["H", "D"]), ("VT", ["H", "D"]),
+                       ("WN", ["H", "D"])]:
+        for k in keys:
+            names.append(f"{comp}.{k}")
+            vals.append(float(hd.HELI[comp][k]))
+    names.append("HELI.M")
+    vals.append(float(hd.HELI["M"]))
+    out["const_names"] = np.array(names)
+    out["const_values"] = np.array(vals)
+    out["IINV"] = np.asarray(hd.HELI["IINV"])
+    out["LG_LOC"] = np.asarray(hd.LG["LOC"])
+    out["wind_mean_ned"] = np.asarray(env.wind_dyn.wind_mean_ned)
+    out["normalizers"] = np.array([env.normalizers[k] for k in "txva"])
+
+    # LookUpTable KATs: the docstring table and the Dryden TEP table.
+    t = ns.lookup.LookUpTable(5, 3)
+    t << 500 << 1000 << 2500 \
+      << 10 << 5 << 15 << 54 \
+      << 20 << 10 << 32 << 65 \
+      << 40 << 28 << 56 << 67 \
+      << 80 << 54 << 99 << 126 \
+      << 160 << 98 << 147 << 598
+    out["lut_doc_table"] = t._data.copy()
+    q = np.array([[42.3, 789.3], [5.0, 100.0], [170.0, 9000.0], [10.0, 500.0], [100.0, 2000.0],
+                  [15.0, 1200.0], [79.9, 2499.0], [0.0, 0.0]])
+    out["lut_doc_queries"] = q
+    # np.float64 keys -> float64 arithmetic; python-float keys -> float32 arithmetic (numpy-2 weak
+    # scalars), which is what the wind path passes (wind_dynamics.py:70,77,96).
+    out["lut_doc_values_f64"] = np.array([float(t.get_value_2D(np.float64(a), np.float64(b))) for a, b in q])
+    out["lut_doc_values"] = np.array([float(t.get_value_2D(float(a), float(b))) for a, b in q])
+    wd = env.wind_dyn
+    out["tep_table"] = wd.TEP._data.copy()
+    tq = []
+    for lvl in [1, 2, 3, 4, 5, 6, 7]:
+        for h in [1000.0, 1200.0, 1750.0, 2000.0, 2500.0, 5000.0, 10000.0, 40000.0, 90000.0]:
+            tq.append((lvl, h))
+    tq = np.array(tq, dtype=np.float64)
+    out["tep_queries"] = tq
+    out["tep_values"] = np.array([float(wd.TEP.get_value_2D(int(a), float(b))) for a, b in tq])
+
+    # Dryden parameters per altitude regime, turbulence level 1 (aw109.yaml ENV).
+    rng = np.random.RandomState(3)
+    cq, cv = [], []
+    for h in [-50.0, 0.0, 5.0, 100.0, 500.0, 999.0, 1000.0, 1000.5, 1200.0, 1500.0, 1999.0,
+              2000.0, 2500.0, 10000.0, 90000.0]:
+        for _ in range(3):
+            v = rng.uniform(-80, 80, size=3)
+            vel_inf = v + wd.wind_mean_ned
+            cq.append([h, *v])
+            cv.append(list(map(float, wd._calc_params(float(h), vel_inf))))
+    out["dryden_queries"] = np.array(cq)
+    out["dryden_values"] = np.array(cv)
+
+    # Terrain ground height (committed x, y) incl. clamps at every edge.
+    pts = [(0, 0), (10.3, -7.7), (-3.2, 3.2), (1000.5, 2000.25), (-3280.0, 3280.0), (3276.0, -3276.0),
+           (3300.0, 0.0), (0.0, 3300.0), (-4000.0, -4000.0), (4000.0, 4000.0), (3277.5, 3277.9),
+           (-3281.0, 12.0), (123.456, -987.654)]
+    rng = np.random.RandomState(4)
+    pts += [tuple(p) for p in rng.uniform(-3500, 3500, size=(40, 2))]
+    gh = []
+    for x, y in pts:
+        hd.state["xyz"] = np.array([x, y, -1000.0], dtype=np.float32)
+        gh.append(float(hd._HelicopterDynamics__get_ground_height_from_hmap()))
+    out["hmap_xy"] = np.array([[np.float32(x), np.float32(y)] for x, y in pts], dtype=np.float64)
+    out["hmap_h"] = np.array(gh)
+
+    xs = np.array([-10.0, -7.0, -3.2, -np.pi, -1e-3, 0.0, 1e-3, 1.0, np.pi, 3.2, 6.3, 7.0, 100.0, 1e4])
+    out["pibound_x"] = xs
+    out["pibound_y"] = ns.utils.pi_bound(xs)
+    return out
+
+
+def gen_trim(ns):
+    rows = {"dt": [], "cond": [], "state": [], "action": [], "obs": [], "state_dots": [], "wind_ned": []}
+    for dt in (0.02, 0.01):
+        for c in TRIM_CASES:
+            env = make_env(ns, dt)
+            env.set_trim_cond(c)
+            obs, _ = env.reset()
+            rows["dt"].append(dt)
+            rows["cond"].append(trim_vec(c))
+            rows["state"].append(np.asarray(env.heli_dyn.state.val, dtype=np.float64))
+            rows["action"].append(np.asarray(env.heli_dyn.action, dtype=np.float64))
+            rows["obs"].append(np.asarray(obs, dtype=np.float64))
+            rows["state_dots"].append(np.asarray(env.heli_dyn.state_dots.val, dtype=np.float64))
+            rows["wind_ned"].append(np.asarray(env.heli_dyn.WIND_NED, dtype=np.float64))
+    out = {k: np.array(v) for k, v in rows.items()}
+    # 2nd-episode reset (F8): trimmed against the last turbulent wind, not the mean wind.
+    env = make_env(ns, 0.02)
+    np.random.seed(11)
+    env.reset()
+    for _ in range(50):
+        env.step(np.zeros(4, np.float32))
+    w = np.asarray(env.heli_dyn.WIND_NED, dtype=np.float64)
+    obs2, _ = env.reset()
+    out["reset2_wind_ned"] = w
+    out["reset2_state"] = np.asarray(env.heli_dyn.state.val, dtype=np.float64)
+    out["reset2_action"] = np.asarray(env.heli_dyn.action, dtype=np.float64)
+    out["reset2_obs"] = np.asarray(obs2, dtype=np.float64)
+    return out
+
+
+def run_scenario(ns, dt, name, cond, kind, max_steps, seed):
+    env = make_env(ns, dt)
+    env.set_trim_cond(cond)
+    np.random.seed(seed)                    # turbulence noise (wind_dynamics.py:52, global RNG)
+    arng = np.random.RandomState(seed + 1000)  # actions
+    obs0, _ = env.reset()
+    rec = {k: [] for k in ["action", "eta", "wind_ned", "state", "wind_state", "obs", "state_dots",
+                           "reward_hover", "success_hover", "reward_ff", "success_ff", "failed",
+                           "successed", "time_up", "terminated", "truncated"]}
+    init = {
+        "state": np.asarray(env.heli_dyn.state.val, dtype=np.float64),
+        "wind_state": np.asarray(env.wind_dyn.state.val, dtype=np.float64),
+        "obs": np.asarray(obs0, dtype=np.float64),
+        "state_dots": np.asarray(env.heli_dyn.state_dots.val, dtype=np.float64),
+        "trim_action": np.asarray(env.heli_dyn.action, dtype=np.float64),
+        "trim_cond": trim_vec(cond),
+    }
+    trim_a = np.asarray(env.heli_dyn.action, dtype=np.float32)
+    for t in range(max_steps):
+        if kind == "zero":
+            a = np.zeros(4, np.float32)
+        elif kind == "uniform":
+            a = arng.uniform(-1, 1, size=4).astype(np.float32)
+        elif kind == "trim":
+            a = trim_a.copy()
+        elif kind == "trim_noise":
+            a = (trim_a + arng.uniform(-0.05, 0.05, size=4)).astype(np.float32)
+        elif kind == "low_collective":
+            a = trim_a.copy()
+            a[0] = -1.0
+            a[1:] += arng.uniform(-0.02, 0.02, size=3).astype(np.float32)
+        else:
+            raise ValueError(kind)
+        obs, rew, term, trunc, info = env.step(a)
+        rff, sff = ff_reward(ns, env)
+        # Hover success_step: recompute through the task's own method (same state).
+        _, shv = ns.tasks.HeliHover._calculate_reward(env)
+        rec["action"].append(a.astype(np.float64))
+        rec["eta"].append(np.asarray(env.wind_dyn.eta, dtype=np.float64))
+        rec["wind_ned"].append(np.asarray(env.heli_dyn.WIND_NED, dtype=np.float64))
+        rec["state"].append(np.asarray(env.heli_dyn.state.val, dtype=np.float64))
+        rec["wind_state"].append(np.asarray(env.wind_dyn.state.val, dtype=np.float64))
+        rec["obs"].append(np.asarray(obs, dtype=np.float64))
+        rec["state_dots"].append(np.asarray(env.heli_dyn.state_dots.val, dtype=np.float64))
+        rec["reward_hover"].append(float(rew))
+        rec["success_hover"].append(bool(shv))
+        rec["reward_ff"].append(float(rff))
+        rec["success_ff"].append(bool(sff))
+        rec["failed"].append(bool(info["failed"]))
+        rec["successed"].append(bool(info["successed"]))
+        rec["time_up"].append(bool(info["time_up"]))
+        rec["terminated"].append(bool(term))
+        rec["truncated"].append(bool(trunc))
+        if term or trunc:
+            break
+    out = {f"{name}/{k}": np.array(v) for k, v in rec.items()}
+    out.update({f"{name}/init_{k}": v for k, v in init.items()})
+    return out
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    ns = refload.load()
+    meta = {"numpy": np.__version__, "generator": "tools/gen_goldens.py",
+            "reference": "ugurcanozalp/heli-gym v2 (/root/reference)"}
+    np.savez_compressed(os.path.join(OUT, "kats.npz"), **gen_kats(ns))
+    np.savez_compressed(os.path.join(OUT, "trim.npz"), **gen_trim(ns))
+    for dt, tag, cap in [(0.02, "0.02", None), (0.01, "0.01", 400)]:
+        out = {}
+        names = []
+        for i, (name, cond, kind, max_steps) in enumerate(SCENARIOS):
+            steps = max_steps if cap is None else min(max_steps, cap)
+            out.update(run_scenario(ns, dt, name, cond, kind, steps, seed=100 + i))
+            names.append(name)
+            print(f"dt={dt} {name}: {len(out[name + '/reward_hover'])} steps", flush=True)
+        out["scenarios"] = np.array(names)
+        out["dt"] = np.array(dt)
+        np.savez_compressed(os.path.join(OUT, f"traj_dt{tag}.npz"), **out)
+    with open(os.path.join(OUT, "META.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
