@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Throughput of the vectorised heli-gym step on MI355X (BASELINE.json metric).
+
+One "step" = one hg_step launch advancing every env of every rank by one env-step (wind RK,
+helicopter RK4, reward, flags, auto-reset) with actions read from HBM.  Workload (BASELINE.json
+configs[2]): 65 536 HeliHover-v0 envs per GPU, Dryden turbulence on (level 1), dt = 0.01 s, fp32,
+U(-1,1) random actions (a Philox-generated bank resident in HBM before timing), auto-reset on.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+Prints ONE JSON line on rank 0.  Envs shard with no data-path collective (weak scaling); the
+optional --gather-obs adds an RCCL all-gather of the observations every step (BASELINE config 5).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "heli-gym_amd"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+# Algorithmic HBM bytes per env-step (DESIGN.md "Roofline"): reads state 27x4 + counters 3x4 +
+# action 16 = 136 B; writes state 108 + counters 12 + obs 68 + reward 4 + terminated/truncated/info 3
+# = 195 B.
+BYTES_PER_ENV_STEP = 136 + 195
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--dt", type=float, default=0.01)
+    ap.add_argument("--task", default="hover", choices=["hover", "forward_flight", "heli"])
+    ap.add_argument("--graph-steps", type=int, default=100, help="steps captured per hipGraph")
+    ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of obs every step")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(dt, task, seconds):
+    """Oracle (C restatement, 1 thread) on a bounded sample of the same workload."""
+    from heligym_amd import config
+    from oracle.oracle import Oracle
+    cfg, doc = config.make_config(task=task, dt=dt)
+    orc = Oracle(cfg, config.load_terrain(doc))
+    tr = orc.trim()
+    t0 = time.perf_counter()
+    n0, _ = orc.rollout(tr, 1, 2000, seed=1)
+    rate0 = n0 / (time.perf_counter() - t0)
+    steps = max(1000, int(rate0 * seconds / 64))
+    t0 = time.perf_counter()
+    n, _ = orc.rollout(tr, 64, steps, seed=2)
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/heli_oracle.c, 64 envs x {steps} steps (dt={dt}, U(-1,1) actions, "
+                      f"turbulence on, auto-reset), {el:.1f} s on 1 host core"}
+
+
+def parity_error(dt, task):
+    """max-abs step() error vs the reference's recorded steps (tests/golden) at this dt."""
+    import numpy as np
+    import torch
+    import golden_cases as gc
+    from heligym_amd import HeliVecEnv
+    tag = {0.01: "0.01", 0.02: "0.02"}.get(round(dt, 6))
+    if tag is None or task not in ("hover", "forward_flight"):
+        return None
+    b = gc.single_step_batch(gc.load(tag), task)
+    env = HeliVecEnv(len(b["state"]), task=task, dt=dt, autoreset=False,
+                     target={"vel": 100.0} if task == "forward_flight" else None)
+    env.set_state(b["state"].astype(np.float32), b["counters"].astype(np.int32))
+    obs, rew, term, trunc, info = env.step(torch.as_tensor(b["actions"].astype(np.float32), device=env.device),
+                                           eta=torch.as_tensor(b["eta"].astype(np.float32), device=env.device))
+    st, _ = env.get_state()
+    obs, st, rew = obs.cpu().numpy(), st.cpu().numpy(), rew.cpu().numpy()
+    term, trunc = term.cpu().numpy(), trunc.cpu().numpy()
+    e_obs = gc.step_errors(obs, b["obs"], gc.OBS_ANGLE_COLS)
+    e_st = gc.step_errors(st[:, :18], b["heli"], gc.HELI_ANGLE_COLS)
+    tol = lambda r: 2e-4 + 2e-5 * np.abs(r)  # noqa: E731
+    flags_ok = bool(np.all(term == b["terminated"]) and np.all(trunc == b["truncated"]))
+    env.close()
+    return {"cases": int(len(b["obs"])), "obs_max_abs": float(e_obs.max()), "state_max_abs": float(e_st.max()),
+            "reward_max_abs": float(np.abs(rew - b["reward"]).max()),
+            "max_err_over_tol": float(max((e_obs / tol(b["obs"])).max(), (e_st / tol(b["heli"])).max())),
+            "flags_identical": flags_ok, "tolerance": "|d| <= 2e-4 + 2e-5|x_ref| (SURVEY 8a-i)"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from heligym_amd import HeliVecEnv
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device(f"cuda:{torch.cuda.current_device()}")
+    N = args.envs
+    env = HeliVecEnv(N, task=args.task, dt=args.dt, seed=1234, autoreset=True, env_offset=rank * N,
+                     device=dev)
+    env.reset()
+
+    B = max(1, args.graph_steps)
+    bank = torch.empty((B, N, 4), dtype=torch.float32, device=dev)
+    for k in range(B):
+        env.random_actions(bank[k], seed=0x5EED, step=k)
+    gathered = None
+    if args.gather_obs and world > 1:
+        gathered = torch.empty((world * N, 17), dtype=torch.float32, device=dev)
+
+    def one_step(k):
+        env.step_async(bank[k % B], with_reset_info=False)
+        if gathered is not None:
+            dist.all_gather_into_tensor(gathered, env.obs)
+
+    # eager warmup, then capture B steps into a hipGraph (launch-bound inner loop)
+    for k in range(args.warmup):
+        one_step(k)
+    torch.cuda.synchronize()
+    graph = None
+    if gathered is None:
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for k in range(B):   # warm the capture stream
+                one_step(k)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for k in range(B):
+                one_step(k)
+        graph.replay()
+        torch.cuda.synchronize()
+
+    reps = max(1, args.steps // B) if graph is not None else args.steps
+    K = reps * B if graph is not None else args.steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    if graph is not None:
+        for _ in range(reps):
+            graph.replay()
+    else:
+        for k in range(K):
+            one_step(k)
+    ev1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    elapsed = ev0.elapsed_time(ev1) * 1e-3
+    el_t = torch.tensor([max(elapsed, 0.0), wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    elapsed = float(el_t[0])
+
+    # per-launch kernel duration on the env's stream (HIP events around single launches)
+    n_ev = 50
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    for j, (a, b) in enumerate(evs):
+        a.record()
+        env.step_async(bank[j % B], with_reset_info=False)
+        b.record()
+    torch.cuda.synchronize()
+    kern_s = sorted(a.elapsed_time(b) * 1e-3 for a, b in evs)[n_ev // 2]
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    total_steps = N * world * K
+    value = total_steps / elapsed
+    achieved = N * BYTES_PER_ENV_STEP / kern_s / 1e9
+    out = {
+        "metric": "env-steps/sec at 65536 envs, 1/2/4/8 MI355X; max-abs step() err vs ref",
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / K * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: U(-1,1) Philox actions (HBM-resident bank of %d steps), Philox turbulence" % B,
+        "config": {"workload": f"{'HeliHover-v0' if args.task == 'hover' else args.task} x {N} envs/GPU, "
+                               f"Dryden turbulence level 1, dt={args.dt}, auto-reset, "
+                               f"{'hipGraph of %d steps' % B if graph is not None else 'eager'}"
+                               + (", RCCL obs all-gather every step" if gathered is not None else ""),
+                   "envs_per_gpu": N, "dt": args.dt, "task": args.task, "parallelism": f"env-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "step_kernel<HOVER>", "kernel_avg_us": kern_s * 1e6,
+                     "bytes_per_env_step": BYTES_PER_ENV_STEP},
+        "wall_s": float(el_t[1]),
+    }
+    if not args.no_parity:
+        try:
+            out["max_abs_step_err"] = parity_error(args.dt, args.task)
+        except Exception as e:   # report, never hide
+            out["max_abs_step_err"] = {"error": repr(e)}
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.dt, args.task, args.cpu_seconds)
+    print(json.dumps(out))
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,842 @@
+// heligym_amd.hip — gfx950 (MI355X) kernels and the C-ABI of include/heligym_amd.h.
+//
+// One launch of `step_kernel` advances N independent helicopters by one env step
+// (Heli.step, heligym/envs/helicopter.py:192-206): Dryden wind RK (k4-only), RK4 of the 18-state
+// helicopter model, task reward, termination flags and same-step auto-reset.  One thread = one
+// env.  Data layout in HBM (all written/read coalesced):
+//   state    [HG_STATE_COLS][N] fp32 SoA  (heli 18 | wind 5 | carry 4)
+//   counters [HG_COUNTER_COLS][N] i32 SoA (episode step, success steps, episode index)
+//   actions  [N,4] fp32 (one float4 per lane)      obs [N,17] fp32 (LDS-staged, float4 stores)
+//   reward [N] fp32, terminated/truncated/info [N] u8
+// Model constants travel as the kernel argument (scalar registers); the terrain map (4 MiB fp32)
+// and the turbulence table stay cache-resident.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/heligym_amd.h"
+#include "physics.h"
+
+using hg::Params;
+using hg::Template;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int32_t fail(int32_t code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(HG_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));         \
+    } while (0)
+
+constexpr int kBlock = 256;
+constexpr int kStateCols = HG_STATE_COLS;
+constexpr int kCtrCols = HG_COUNTER_COLS;
+
+__constant__ float c_tep[8][13] = HG_TEP_TABLE;
+const float h_tep[8][13] = HG_TEP_TABLE;
+
+// ------------------------------------------------------------------------------ Philox4x32-10
+struct U4 {
+    uint32_t x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+        const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) {   // (0, 1)
+    return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
+}
+
+// ------------------------------------------------------------------------------ kernels
+
+struct StepArgs {
+    float* state;
+    int32_t* counters;
+    const float2* hmap;
+    const float* actions;
+    float* obs;
+    float* reward;
+    uint8_t* terminated;
+    uint8_t* truncated;
+    uint8_t* info;
+    const float* eta;
+    int32_t* reset_count;
+    int32_t* reset_index;
+    float* final_obs;
+    int64_t n;
+    uint64_t seed;
+    int64_t env_offset;
+};
+
+template <int TASK>
+__global__ __launch_bounds__(kBlock) void step_kernel(const Params<float> P, const Template<float> T,
+                                                      const StepArgs a) {
+    __shared__ float s_obs[kBlock * HG_N_OBS];
+    const int tid = threadIdx.x;
+    const int64_t blk0 = (int64_t)blockIdx.x * kBlock;
+    const int64_t i = blk0 + tid;
+    const int64_t n = a.n;
+    const bool active = i < n;
+    const int64_t ii = active ? i : 0;   // inactive lanes compute on env 0 and store nothing
+
+    float hs[18], ws[5], carry[4];
+#pragma unroll
+    for (int c = 0; c < 18; ++c) hs[c] = a.state[c * n + ii];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) ws[c] = a.state[(18 + c) * n + ii];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) carry[c] = a.state[(23 + c) * n + ii];
+    int32_t step = a.counters[ii], succ = a.counters[n + ii], epi = a.counters[2 * n + ii];
+    const float4 act = reinterpret_cast<const float4*>(a.actions)[ii];
+
+    // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
+    float eta[3];
+    if (a.eta) {
+        eta[0] = a.eta[3 * ii + 0];
+        eta[1] = a.eta[3 * ii + 1];
+        eta[2] = a.eta[3 * ii + 2];
+    } else {
+        const uint64_t gid = (uint64_t)(a.env_offset + ii);
+        const U4 r = philox(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)epi},
+                            (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+        float sn, cs;
+        const float r0 = sqrtf(-2.f * __logf(u01(r.x)));
+        __sincosf(6.28318530717958648f * u01(r.y), &sn, &cs);
+        const float r1 = sqrtf(-2.f * __logf(u01(r.z)));
+        eta[0] = r0 * cs * P.eta_norm;
+        eta[1] = r0 * sn * P.eta_norm;
+        eta[2] = r1 * __cosf(6.28318530717958648f * u01(r.w)) * P.eta_norm;
+    }
+
+    // ground height under the committed position (F6), wind step (Heli.step :195-199)
+    const hg::Ground<float> h_c = hg::ground_height(P, a.hmap, hs[15], hs[16]);
+    float W[3];
+    hg::wind_step(P, c_tep, ws, carry, eta, W);
+
+    // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
+    const hg::Controls<float> u = hg::controls(P, act.x, act.y, act.z, act.w);
+    float k[18], acc[18], st[18], obs[17];
+    hg::dynamics<false>(P, hs, u, W, h_c, k, obs);
+#pragma unroll
+    for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
+    hg::dynamics<false>(P, st, u, W, h_c, k, obs);
+#pragma unroll
+    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
+    hg::dynamics<false>(P, st, u, W, h_c, k, obs);
+#pragma unroll
+    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.dt; }
+    hg::dynamics<true>(P, st, u, W, h_c, k, obs);
+#pragma unroll
+    for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
+    // step_after (helicopter_dynamics.py:73-77)
+    hs[2] = hg::pi_bound(hs[2]);
+    hs[3] = hg::pi_bound(hs[3]);
+    hs[4] = hg::pi_bound(hs[4]);
+    hs[5] = hg::pi_bound(hs[5]);
+    hs[12] = hg::pi_bound(hs[12]);
+    hs[13] = hg::pi_bound(hs[13]);
+    hs[14] = hg::pi_bound(hs[14]);
+
+    // reward (helicopter_with_tasks.py) and flags (helicopter.py:201-205, 219-240)
+    bool success_step = false;
+    float rew = 0.f;
+    if (TASK == HG_TASK_HOVER) rew = hg::reward_hover(P, hs, k, &success_step);
+    if (TASK == HG_TASK_FORWARD_FLIGHT) rew = hg::reward_forward(P, hs, k, &success_step);
+    const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
+    step += 1;
+    const bool failed = hg::is_failed(P, hs, k, h_post);
+    const bool successed = succ >= P.success_steps;   // successed_time before this step's add
+    const bool time_up = step >= P.time_up_steps;
+    const bool term = failed || successed;
+    const bool done = term || time_up;
+    succ += success_step ? 1 : 0;
+
+    if (active) {
+        a.reward[i] = rew;
+        a.terminated[i] = term;
+        a.truncated[i] = time_up;
+        if (a.info)
+            a.info[i] = (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
+                                  (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0));
+    }
+
+    // same-step auto-reset with a wave-ballot compaction of the finished envs
+    const bool do_reset = P.autoreset && active && done;
+    if (P.autoreset && a.reset_count) {
+        const unsigned long long mask = __ballot(do_reset);
+        if (mask) {
+            const int lane = tid & 63;
+            const int leader = __ffsll((long long)mask) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(a.reset_count, __popcll(mask));
+            base = __shfl(base, leader);
+            if (do_reset) {
+                const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
+                if (a.reset_index) a.reset_index[slot] = (int32_t)i;
+                if (a.final_obs) {
+#pragma unroll
+                    for (int c = 0; c < 17; ++c) a.final_obs[(int64_t)slot * 17 + c] = obs[c];
+                }
+            }
+        }
+    }
+    if (do_reset) {
+#pragma unroll
+        for (int c = 0; c < 18; ++c) hs[c] = T.heli[c];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) ws[c] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) carry[c] = T.carry[c];
+#pragma unroll
+        for (int c = 0; c < 17; ++c) obs[c] = T.obs[c];
+        step = 0;
+        succ = 0;
+        epi += 1;
+    } else {
+        carry[0] = obs[4];
+        carry[1] = obs[5];
+        carry[2] = obs[6];
+        carry[3] = obs[16];
+    }
+
+    if (active) {
+#pragma unroll
+        for (int c = 0; c < 18; ++c) a.state[c * n + i] = hs[c];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) a.state[(18 + c) * n + i] = ws[c];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a.state[(23 + c) * n + i] = carry[c];
+        a.counters[i] = step;
+        a.counters[n + i] = succ;
+        a.counters[2 * n + i] = epi;
+    }
+
+    // observations: stage through LDS (stride 17 is bank-conflict free) -> contiguous float4 stores
+#pragma unroll
+    for (int c = 0; c < 17; ++c) s_obs[tid * 17 + c] = obs[c];
+    __syncthreads();
+    const int64_t nb = (n - blk0) < kBlock ? (n - blk0) : kBlock;
+    const int cnt = (int)nb * 17;
+    float* out = a.obs + blk0 * 17;
+    const int n4 = cnt >> 2;
+    for (int j = tid; j < n4; j += kBlock)
+        reinterpret_cast<float4*>(out)[j] = reinterpret_cast<const float4*>(s_obs)[j];
+    for (int j = (n4 << 2) + tid; j < cnt; j += kBlock) out[j] = s_obs[j];
+}
+
+// Heli.reset for masked envs (helicopter.py:208-217)
+__global__ __launch_bounds__(kBlock) void reset_kernel(const Template<float> T, float* state, int32_t* counters,
+                                                       const uint8_t* mask, float* obs, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    if (mask && !mask[i]) return;
+#pragma unroll
+    for (int c = 0; c < 18; ++c) state[c * n + i] = T.heli[c];
+#pragma unroll
+    for (int c = 0; c < 5; ++c) state[(18 + c) * n + i] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) state[(23 + c) * n + i] = T.carry[c];
+    counters[i] = 0;
+    counters[n + i] = 0;
+    counters[2 * n + i] += 1;
+    if (obs) {
+#pragma unroll
+        for (int c = 0; c < 17; ++c) obs[i * 17 + c] = T.obs[c];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void init_kernel(const Template<float> T, float* state, int32_t* counters,
+                                                      int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    for (int c = 0; c < 18; ++c) state[c * n + i] = T.heli[c];
+    for (int c = 0; c < 5; ++c) state[(18 + c) * n + i] = 0.f;
+    for (int c = 0; c < 4; ++c) state[(23 + c) * n + i] = T.carry[c];
+    counters[i] = 0;
+    counters[n + i] = 0;
+    counters[2 * n + i] = 0;
+}
+
+// SoA <-> [N, cols] record transposes for get/set_state
+__global__ void soa_to_rows(const float* soa, float* rows, int cols, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    for (int c = 0; c < cols; ++c) rows[i * cols + c] = soa[c * n + i];
+}
+__global__ void rows_to_soa(const float* rows, float* soa, int cols, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    for (int c = 0; c < cols; ++c) soa[c * n + i] = rows[i * cols + c];
+}
+__global__ void isoa_to_rows(const int32_t* soa, int32_t* rows, int cols, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    for (int c = 0; c < cols; ++c) rows[i * cols + c] = soa[c * n + i];
+}
+__global__ void irows_to_soa(const int32_t* rows, int32_t* soa, int cols, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    for (int c = 0; c < cols; ++c) soa[c * n + i] = rows[i * cols + c];
+}
+
+__global__ __launch_bounds__(kBlock) void random_actions_kernel(float* act, int64_t n, int64_t env_offset,
+                                                                uint64_t seed, uint64_t step, float lo, float hi) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t gid = (uint64_t)(env_offset + i);
+    const U4 r = philox(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)(step >> 32)},
+                        (uint32_t)seed ^ 0xA511E9B3u, (uint32_t)(seed >> 32) ^ 0x63D83595u);
+    const float w = hi - lo;
+    reinterpret_cast<float4*>(act)[i] =
+        make_float4(lo + w * u01(r.x), lo + w * u01(r.y), lo + w * u01(r.z), lo + w * u01(r.w));
+}
+
+// ------------------------------------------------------------------------------ host model
+
+constexpr double kD2R = 3.14159265358979323846 / 180.0;
+
+// First n at which the reference's float accumulator crosses its threshold
+// (helicopter.py:193 `time_counter += DT` vs `> max_time`; :205 `successed_time += DT` vs `>=`).
+int32_t first_step_above(double dt, double thr, bool strict) {
+    double t = 0.0;
+    int64_t k = 0;
+    while (k < (int64_t)2000000000) {
+        if (strict ? (t > thr) : (t >= thr)) return (int32_t)k;
+        t += dt;
+        ++k;
+    }
+    return INT32_MAX;
+}
+
+template <typename R>
+Params<R> derive(const hg_config& c, int rows, int cols) {
+    const hg_airframe& a = c.af;
+    Params<R> P;
+    memset(&P, 0, sizeof(P));
+    const double dt = c.dt;
+    P.dt = (R)dt;
+    P.half_dt = (R)(0.5 * dt);
+    P.dt6 = (R)(0.16666666666666666 * dt);
+    // helicopter_dynamics.py:414-422
+    P.coll0 = (R)(kD2R * (a.COL_OS + 0.5 * (a.COL_H + a.COL_L)));
+    P.coll1 = (R)(kD2R * 0.5 * (a.COL_H - a.COL_L));
+    P.lon0 = (R)(kD2R * 0.5 * (a.LON_H + a.LON_L));
+    P.lon1 = (R)(kD2R * 0.5 * (a.LON_H - a.LON_L));
+    P.lat0 = (R)(kD2R * 0.5 * (a.LAT_H + a.LAT_L));
+    P.lat1 = (R)(kD2R * 0.5 * (a.LAT_H - a.LAT_L));
+    P.ped0 = (R)(kD2R * (a.PED_OS + 0.5 * (a.PED_H + a.PED_L)));
+    P.ped1 = (R)(kD2R * 0.5 * (a.PED_H - a.PED_L));
+    // :160-165
+    P.lapse_t0 = (R)(a.env_LAPSE / a.env_T0);
+    P.ro_sea = (R)a.env_RO_SEA;
+    P.rho_exp = (R)(a.env_GRAV / (a.env_LAPSE * a.env_R) - 1.0);
+    // :107-154
+    const double mass = a.WT / a.env_GRAV;
+    P.wt = (R)a.WT;
+    P.inv_mass = (R)(1.0 / mass);
+    P.p_loss = (R)(550.0 * a.HP_LOSS);
+    P.vtrans = (R)a.VTRANS;
+    P.wl_cg_ft = (R)(a.WL_CG / 12.0);
+    const double mr_H = (a.mr_WL - a.WL_CG) / 12, mr_D = (a.mr_FS - a.FS_CG) / 12;
+    const double fus_H = (a.fus_WL - a.WL_CG) / 12, fus_D = (a.fus_FS - a.FS_CG) / 12;
+    const double ht_H = (a.ht_WL - a.WL_CG) / 12, ht_D = (a.ht_FS - a.FS_CG) / 12;
+    const double vt_H = (a.vt_WL - a.WL_CG) / 12, vt_D = (a.vt_FS - a.FS_CG) / 12;
+    const double tr_H = (a.tr_WL - a.WL_CG) / 12, tr_D = (a.tr_FS - a.FS_CG) / 12;
+    const double mr_OM = a.mr_RPM * 2 * M_PI / 60, mr_VT = a.mr_R * mr_OM;
+    const double mr_FR = a.mr_CD0 * a.mr_R * a.mr_B * a.mr_C;
+    const double mr_SOL = a.mr_B * a.mr_C / (a.mr_R * M_PI);
+    const double mr_ASIG = a.mr_A * mr_SOL;
+    P.mr_H = (R)mr_H; P.mr_D = (R)mr_D; P.mr_IS = (R)a.mr_IS; P.mr_K1 = (R)a.mr_K1; P.mr_R = (R)a.mr_R;
+    P.mr_OMEGA = (R)mr_OM; P.mr_inv_OMEGA = (R)(1.0 / mr_OM);
+    P.mr_VTIP = (R)mr_VT; P.mr_inv_VTIP = (R)(1.0 / mr_VT);
+    P.mr_tw75 = (R)(0.75 * a.mr_TWST); P.mr_tw50 = (R)(0.5 * a.mr_TWST);
+    P.mr_two3_vtip = (R)(0.66667 * mr_VT);
+    P.mr_gam_dro = (R)(a.mr_A * a.mr_C * pow(a.mr_R, 4) / a.mr_IB * mr_OM / 16 * (1 + 8.0 / 3 * a.mr_E / a.mr_R));
+    P.mr_kc_num = (R)(0.75 * mr_OM * a.mr_E / a.mr_R);
+    P.mr_DL_DB1 = (R)(a.mr_B / 2 * (1.5 * a.mr_IB * a.mr_E / a.mr_R * mr_OM * mr_OM));
+    P.mr_DL_DA1_dro = (R)(0.5 * a.mr_A * a.mr_B * a.mr_C * a.mr_R * mr_VT * mr_VT * a.mr_E / 6);
+    P.mr_coef = (R)(0.25 * mr_VT * a.mr_R * a.mr_A * a.mr_B * a.mr_C);
+    P.mr_inflow = (R)(0.75 * M_PI / a.mr_R);
+    P.mr_inv_thr_den = (R)(1.0 / (2 * M_PI * a.mr_R * a.mr_R));
+    P.mr_inv_ct_den = (R)(1.0 / (M_PI * a.mr_R * a.mr_R * mr_VT * mr_VT));
+    P.mr_prof = (R)(0.5 * (mr_FR / 4) * mr_VT);
+    P.mr_vtip2 = (R)(mr_VT * mr_VT);
+    P.mr_2_vtip = (R)(2.0 / mr_VT);
+    P.mr_8_asig = (R)(8.0 / mr_ASIG);
+    const double tr_OM = a.tr_RPM * 2 * M_PI / 60, tr_VT = a.tr_R * tr_OM;
+    P.tr_H = (R)tr_H; P.tr_D = (R)tr_D; P.tr_OMEGA = (R)tr_OM;
+    P.tr_VTIP = (R)tr_VT; P.tr_inv_VTIP = (R)(1.0 / tr_VT);
+    P.tr_tw75 = (R)(0.75 * a.tr_TWST); P.tr_tw50 = (R)(0.5 * a.tr_TWST);
+    P.tr_two3_vtip = (R)(0.66667 * tr_VT);
+    P.tr_coef = (R)(0.25 * tr_VT * a.tr_R * a.tr_A * a.tr_B * a.tr_C);
+    P.tr_inflow = (R)(0.5 * 0.75 * M_PI / a.tr_R);   // :285 halves the TR inflow rate
+    P.tr_inv_thr_den = (R)(1.0 / (2 * M_PI * a.tr_R * a.tr_R));
+    P.fus_H = (R)fus_H; P.fus_XUU = (R)a.fus_XUU; P.fus_YVV = (R)a.fus_YVV; P.fus_ZWW = (R)a.fus_ZWW;
+    P.fus_COR = (R)a.fus_COR; P.fus_dfw_k = (R)(mr_H - fus_H); P.fus_dfw_c = (R)(fus_D - mr_D);
+    P.ht_D = (R)ht_D; P.ht_ZUU = (R)a.ht_ZUU; P.ht_ZUW = (R)a.ht_ZUW; P.ht_ZMAX = (R)a.ht_ZMAX;
+    P.ht_dw_k = (R)(mr_H - ht_H); P.ht_dw_c = (R)(ht_D - mr_D - a.mr_R);
+    P.vt_H = (R)vt_H; P.vt_D = (R)vt_D; P.vt_YUU = (R)a.vt_YUU; P.vt_YUV = (R)a.vt_YUV; P.vt_YMAX = (R)a.vt_YMAX;
+    P.wn_ZUU = (R)a.wn_ZUU; P.wn_ZUW = (R)a.wn_ZUW; P.wn_ZMAX = (R)a.wn_ZMAX;
+    P.wn_on = a.wn_ZUW != 0.0;   // :367
+    P.lg_K = (R)a.lg_K; P.lg_C = (R)a.lg_C;
+    const double loc[3][3] = {{-(a.lg_FS_N - a.FS_CG), 0.0, -(a.lg_WL - a.WL_CG)},
+                              {-(a.lg_FS_MN - a.FS_CG), a.lg_BL_MN, -(a.lg_WL - a.WL_CG)},
+                              {-(a.lg_FS_MN - a.FS_CG), -a.lg_BL_MN, -(a.lg_WL - a.WL_CG)}};
+    for (int g = 0; g < 3; ++g)
+        for (int j = 0; j < 3; ++j) P.lg_loc[g][j] = (R)(loc[g][j] / 12.0);   // :123-126
+    // inertia and inverse (:151-154)
+    const double Ix = a.IX, Iy = a.IY, Iz = a.IZ, Ixz = -a.IXZ;
+    const double det = Ix * Iz - Ixz * Ixz;
+    P.Ixx = (R)Ix; P.Iyy = (R)Iy; P.Izz = (R)Iz; P.Ixz = (R)Ixz;
+    P.Ji00 = (R)(Iz / det); P.Ji02 = (R)(-Ixz / det); P.Ji11 = (R)(1.0 / Iy);
+    P.Ji20 = (R)(-Ixz / det); P.Ji22 = (R)(Ix / det);
+    // terrain (:167-172)
+    P.hm_sx = (R)(rows / a.env_NS_MAX);
+    P.hm_sy = (R)(cols / a.env_EW_MAX);
+    P.hm_cx = (R)(rows / 2);
+    P.hm_cy = (R)(cols / 2);
+    P.hm_rows = rows;
+    P.hm_cols = cols;
+    P.ns_half = (R)(a.env_NS_MAX / 2);
+    P.ew_half = (R)(a.env_EW_MAX / 2);
+    // wind (wind_dynamics.py:21-28, 56)
+    const double wdir = a.env_WIND_DIR_deg * kD2R;
+    P.wm[0] = (R)(a.env_WIND_SPD * (double)(float)cos(wdir));
+    P.wm[1] = (R)(a.env_WIND_SPD * (double)(float)sin(wdir));
+    P.wm[2] = (R)0;
+    P.wind_dir_cos = (R)cos(wdir);
+    P.wind_dir_sin = (R)sin(wdir);
+    const double w20 = a.env_TURB_LVL / 7.0 * 88.61;
+    P.w20 = (R)w20;
+    P.sigma_low = (R)(0.1 * w20);
+    P.turb_level = (R)a.env_TURB_LVL;
+    P.eta_norm = (R)(1.0 / sqrt(dt));
+    // task (helicopter.py:63-68, helicopter_with_tasks.py:33, 87-88)
+    const double n_t = sqrt(2 * a.mr_R / a.env_GRAV), n_x = 2 * a.mr_R, n_v = sqrt(2 * a.mr_R * a.env_GRAV);
+    P.n_t = (R)n_t; P.n_t2 = (R)(n_t * n_t);
+    P.inv_n_x = (R)(1.0 / n_x); P.inv_n_v = (R)(1.0 / n_v); P.inv_n_a = (R)(1.0 / a.env_GRAV);
+    P.tgt_n[0] = (R)(c.target.north_loc / n_x);
+    P.tgt_n[1] = (R)(c.target.east_loc / n_x);
+    P.tgt_n[2] = (R)(-c.target.sea_alt / n_x);
+    P.vel_tgt_n = (R)(c.target.vel / n_v);
+    P.dwn_tgt_n = (R)(-c.target.sea_alt / n_x);
+    P.fail_zdot = (R)(mr_VT * 0.05);
+    P.fail_ang = (R)(60 * kD2R);
+    P.task = c.task;
+    P.time_up_steps = first_step_above(dt, c.max_time, true);
+    P.success_steps = first_step_above(dt, c.max_time / 4, false);
+    P.autoreset = c.autoreset ? 1 : 0;
+    return P;
+}
+
+// helicopter_dynamics.py:557-576 (__trim_fcn): normalised derivatives at the trial point x.  The
+// reference writes the trial point into its float32 state array, so it is rounded to float here.
+void trim_fcn(const Params<double>& P, const double base[18], const double x[16], const double W[3],
+              const hg::Ground<double>& h_c, double y[16], double* s_out, double* d_out, double* obs) {
+    double s[18];
+    memcpy(s, base, sizeof(s));
+    s[0] = (float)(x[0] * P.mr_VTIP);
+    s[1] = (float)(x[1] * P.tr_VTIP);
+    s[4] = (float)x[2];
+    s[5] = (float)x[3];
+    for (int i = 0; i < 3; ++i) {
+        s[6 + i] = (float)(x[4 + i] * P.mr_VTIP);
+        s[9 + i] = (float)(x[7 + i] * P.mr_OMEGA);
+    }
+    s[12] = (float)x[10];
+    s[13] = (float)x[11];
+    const hg::Controls<double> u = hg::controls(P, x[12], x[13], x[14], x[15]);
+    double d[18], ob[17];
+    hg::dynamics<true>(P, s, u, W, h_c, d, ob);
+    y[0] = d[0] / P.mr_VTIP;
+    y[1] = d[1] / P.tr_VTIP;
+    y[2] = d[4];
+    y[3] = d[5];
+    for (int i = 0; i < 3; ++i) {
+        y[4 + i] = d[6 + i] / P.mr_VTIP;
+        y[7 + i] = d[9 + i] / P.mr_OMEGA;
+        y[10 + i] = d[12 + i];
+        y[13 + i] = d[15 + i] / P.mr_R;
+    }
+    if (s_out) memcpy(s_out, s, sizeof(s));
+    if (d_out) memcpy(d_out, d, sizeof(d));
+    if (obs) memcpy(obs, ob, sizeof(ob));
+}
+
+// np.linalg.inv(dydx) @ r via Gauss-Jordan with partial pivoting
+bool solve16(double A[16][16], const double r[16], double v[16]) {
+    double M[16][17];
+    for (int i = 0; i < 16; ++i) {
+        for (int j = 0; j < 16; ++j) M[i][j] = A[i][j];
+        M[i][16] = r[i];
+    }
+    for (int c = 0; c < 16; ++c) {
+        int p = c;
+        for (int i = c + 1; i < 16; ++i)
+            if (fabs(M[i][c]) > fabs(M[p][c])) p = i;
+        if (M[p][c] == 0.0 || !std::isfinite(M[p][c])) return false;
+        if (p != c)
+            for (int j = 0; j < 17; ++j) std::swap(M[c][j], M[p][j]);
+        const double piv = M[c][c];
+        for (int j = c; j < 17; ++j) M[c][j] /= piv;
+        for (int i = 0; i < 16; ++i) {
+            if (i == c) continue;
+            const double f = M[i][c];
+            if (f != 0.0)
+                for (int j = c; j < 17; ++j) M[i][j] -= f * M[c][j];
+        }
+    }
+    for (int i = 0; i < 16; ++i) v[i] = M[i][16];
+    return true;
+}
+
+// HelicopterDynamics.trim (helicopter_dynamics.py:491-555), fp64 Newton with a central-difference
+// Jacobian and step halving, identical iteration logic to the reference.
+int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond& tc, const double W[3],
+                hg_trim_result* out) {
+    double base[18] = {0};
+    base[14] = (float)tc.yaw;
+    base[2] = (float)tc.psi_mr;
+    base[3] = (float)tc.psi_tr;
+    base[15] = (float)tc.xy[0];
+    base[16] = (float)tc.xy[1];
+    const hg::Ground<double> h_c = hg::ground_height(P, hmap, base[15], base[16]);
+    base[17] = (float)(-(h_c.h() + P.wl_cg_ft) - tc.gr_alt);
+    double yt[16] = {0};
+    yt[12] = (float)tc.yaw_rate;
+    for (int i = 0; i < 3; ++i) yt[13 + i] = (float)tc.ned_vel[i] / (float)P.mr_R;
+    double x[16] = {0.05f, 0.05f, 0, 0, 0, 0, 0, 0, 0, (float)tc.yaw_rate, -0.01f, 0.01f, 0, 0, 0, 0};
+    for (int i = 0; i < 3; ++i) x[4 + i] = (float)tc.ned_vel[i] / (float)P.mr_VTIP;
+    const double eps = 1e-4;
+    double y[16], tol = 0;
+    trim_fcn(P, base, x, W, h_c, y, nullptr, nullptr, nullptr);
+    for (int i = 0; i < 16; ++i) tol += (y[i] - yt[i]) * (y[i] - yt[i]);
+    int it = 0;
+    while (tol > eps) {
+        double J[16][16], yp[16], ym[16], xp[16], xm[16], r[16], dir[16];
+        for (int i = 0; i < 16; ++i) {
+            memcpy(xp, x, sizeof(x));
+            memcpy(xm, x, sizeof(x));
+            xp[i] += eps;
+            xm[i] -= eps;
+            trim_fcn(P, base, xp, W, h_c, yp, nullptr, nullptr, nullptr);
+            trim_fcn(P, base, xm, W, h_c, ym, nullptr, nullptr, nullptr);
+            for (int k = 0; k < 16; ++k) J[k][i] = (yp[k] - ym[k]) / (2 * eps);
+        }
+        for (int k = 0; k < 16; ++k) r[k] = y[k] - yt[k];
+        if (!solve16(J, r, dir)) return fail(HG_E_TRIM, "trim: singular Jacobian");
+        double step = 1.0, xn[16], yn[16], tn = 0;
+        int j;
+        for (j = 0; j < 10; ++j) {
+            for (int k = 0; k < 16; ++k) xn[k] = x[k] - step * dir[k];
+            trim_fcn(P, base, xn, W, h_c, yn, nullptr, nullptr, nullptr);
+            tn = 0;
+            for (int k = 0; k < 16; ++k) tn += (yn[k] - yt[k]) * (yn[k] - yt[k]);
+            step *= 0.5;
+            if (tn < tol) break;
+        }
+        if (j >= 9) break;   // :540
+        memcpy(x, xn, sizeof(x));
+        memcpy(y, yn, sizeof(y));
+        tol = tn;
+        if (++it > 200)   // the reference gives up after 5 s (:543-544)
+            return fail(HG_E_TRIM, "Trim failed, please try a better trim condition!");
+    }
+    trim_fcn(P, base, x, W, h_c, y, out->state, out->state_dots, out->obs);
+    for (int i = 0; i < 4; ++i) out->action[i] = x[12 + i];
+    out->residual = tol;
+    out->iterations = it;
+    const hg::Ground<double> h_post = hg::ground_height(P, hmap, out->state[15], out->state[16]);
+    out->failed = hg::is_failed(P, out->state, out->state_dots, h_post) ? 1 : 0;
+    return HG_OK;
+}
+
+int32_t check_config(const hg_config* c, int32_t rows, int32_t cols) {
+    if (!c) return fail(HG_E_INVALID, "config is NULL");
+    if (!(c->dt > 0) || !std::isfinite(c->dt)) return fail(HG_E_INVALID, "dt must be > 0");
+    if (!(c->max_time > 0)) return fail(HG_E_INVALID, "max_time must be > 0");
+    if (c->task < HG_TASK_HELI || c->task > HG_TASK_FORWARD_FLIGHT) return fail(HG_E_INVALID, "bad task");
+    if (c->af.env_TURB_LVL < 0 || c->af.env_TURB_LVL > 7) return fail(HG_E_INVALID, "TURB_LVL must be 0..7");
+    if (rows < 2 || cols < 2 || rows != cols)
+        return fail(HG_E_INVALID, "terrain must be a square map of at least 2x2 samples");
+    return HG_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------ handle
+
+struct hg_env {
+    hg_config cfg;
+    int64_t n = 0;
+    int rows = 0, cols = 0;
+    std::vector<float2> hmap_host;   // {hi, lo} split of the fp64 heights
+    float2* hmap = nullptr;
+    float* state = nullptr;
+    int32_t* counters = nullptr;
+    Params<float> Pf;
+    Params<double> Pd;
+    Template<float> tmpl;
+    hg_trim_result trim;
+};
+
+static int32_t build_template(hg_env* e) {
+    const double W[3] = {e->Pd.wm[0], e->Pd.wm[1], e->Pd.wm[2]};   // helicopter.py:55 (mean wind)
+    hg_trim_result r;
+    memset(&r, 0, sizeof(r));
+    const int32_t rc = do_trim(e->Pd, e->hmap_host.data(), e->cfg.trim, W, &r);
+    if (rc != HG_OK) return rc;
+    e->trim = r;
+    for (int c = 0; c < 18; ++c) e->tmpl.heli[c] = (float)r.state[c];
+    for (int c = 0; c < 17; ++c) e->tmpl.obs[c] = (float)r.obs[c];
+    e->tmpl.carry[0] = (float)r.obs[4];
+    e->tmpl.carry[1] = (float)r.obs[5];
+    e->tmpl.carry[2] = (float)r.obs[6];
+    e->tmpl.carry[3] = (float)r.obs[16];
+    return HG_OK;
+}
+
+static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+extern "C" {
+
+int32_t hg_abi_version(void) { return HG_ABI_VERSION; }
+
+const char* hg_last_error(void) { return g_last_error.c_str(); }
+
+void hg_default_config(hg_config* c) {
+    if (!c) return;
+    memset(c, 0, sizeof(*c));
+    hg_airframe& a = c->af;
+    // aw109.yaml:2-101
+    a.env_R = 1716.49; a.env_T0 = 518.4; a.env_LAPSE = 0.0035662; a.env_RO_SEA = 0.0023769;
+    a.env_GRAV = 32.2; a.env_MAX_GR_ALT = 8809.0551; a.env_NS_MAX = 6561.6798; a.env_EW_MAX = 6561.6798;
+    a.env_WIND_DIR_deg = 45.0; a.env_WIND_SPD = 20.0; a.env_TURB_LVL = 1;
+    a.HP_LOSS = 90; a.VTRANS = 50; a.FS_CG = 132.7; a.WL_CG = 38.5; a.WT = 5401;
+    a.IX = 1590; a.IY = 6761; a.IZ = 6407; a.IXZ = 598;
+    a.COL_OS = 6; a.COL_L = -2; a.COL_H = 15; a.LON_L = -12; a.LON_H = 12; a.LAT_L = -10; a.LAT_H = 10;
+    a.PED_OS = 15; a.PED_L = -15; a.PED_H = 15;
+    a.mr_FS = 132.4; a.mr_WL = 98.2; a.mr_IS = 0.11; a.mr_E = 0.5; a.mr_IB = 212; a.mr_R = 18; a.mr_A = 5.8;
+    a.mr_RPM = 385; a.mr_CD0 = 0.009; a.mr_B = 4; a.mr_C = 1.1; a.mr_TWST = -0.105; a.mr_K1 = 0.096;
+    a.tr_FS = 391; a.tr_WL = 70; a.tr_R = 3.1; a.tr_A = 4.2; a.tr_C = 0.6525; a.tr_RPM = 2080; a.tr_CD0 = 0.009;
+    a.tr_TWST = -0.137; a.tr_B = 2;
+    a.fus_FS = 132; a.fus_WL = 38; a.fus_XUU = -10.8; a.fus_YVV = -167; a.fus_ZWW = -85; a.fus_COR = 3;
+    a.ht_FS = 330; a.ht_WL = 54; a.ht_ZUU = 0.4; a.ht_ZUW = -34.0; a.ht_ZMAX = -22.0;
+    a.vt_FS = 380; a.vt_WL = 80; a.vt_YUU = 3.3; a.vt_YUV = -47; a.vt_YMAX = -17;
+    a.wn_FS = 0; a.wn_WL = 0; a.wn_ZUU = 0; a.wn_ZUW = 0; a.wn_ZMAX = 0; a.wn_B = 1;
+    a.lg_K = 30000; a.lg_C = 2000; a.lg_BL_MN = 42; a.lg_FS_MN = 187; a.lg_FS_N = 40; a.lg_WL = -22;
+    // helicopter.py:18-44, helicopter_with_tasks.py:9-22
+    c->trim.gr_alt = 100.0;
+    c->target.sea_alt = 4000.0;
+    c->dt = 1.0 / 50.0;
+    c->max_time = 40.0;
+    c->task = HG_TASK_HOVER;
+    c->autoreset = 1;
+}
+
+static std::vector<float2> split_terrain(const double* t, int32_t rows, int32_t cols) {
+    std::vector<float2> v((size_t)rows * cols);
+    for (size_t k = 0; k < v.size(); ++k) {
+        const float hi = (float)t[k];
+        v[k] = make_float2(hi, (float)(t[k] - (double)hi));
+    }
+    return v;
+}
+
+int32_t hg_trim(const hg_config* cfg, const double* terrain_ft, int32_t rows, int32_t cols,
+                const double wind_ned[3], hg_trim_result* out) {
+    int32_t rc = check_config(cfg, rows, cols);
+    if (rc != HG_OK) return rc;
+    if (!terrain_ft || !out) return fail(HG_E_INVALID, "terrain/out is NULL");
+    const Params<double> P = derive<double>(*cfg, rows, cols);
+    double W[3] = {P.wm[0], P.wm[1], P.wm[2]};
+    if (wind_ned) { W[0] = wind_ned[0]; W[1] = wind_ned[1]; W[2] = wind_ned[2]; }
+    memset(out, 0, sizeof(*out));
+    const std::vector<float2> hm = split_terrain(terrain_ft, rows, cols);
+    return do_trim(P, hm.data(), cfg->trim, W, out);
+}
+
+int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, int32_t cols, int64_t num_envs,
+                  hg_env** out) {
+    if (!out) return fail(HG_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int32_t rc = check_config(cfg, rows, cols);
+    if (rc != HG_OK) return rc;
+    if (!terrain_ft) return fail(HG_E_INVALID, "terrain is NULL");
+    if (num_envs < 1 || num_envs > ((int64_t)1 << 31) - kBlock)
+        return fail(HG_E_INVALID, "num_envs must be in [1, 2^31 - 256)");
+    hg_env* e = new hg_env();
+    e->cfg = *cfg;
+    e->n = num_envs;
+    e->rows = rows;
+    e->cols = cols;
+    e->hmap_host = split_terrain(terrain_ft, rows, cols);
+    e->Pd = derive<double>(*cfg, rows, cols);
+    e->Pf = derive<float>(*cfg, rows, cols);
+    rc = build_template(e);
+    if (rc != HG_OK) { delete e; return rc; }
+    auto cleanup = [&](hipError_t err, const char* what) {
+        hipFree(e->hmap); hipFree(e->state); hipFree(e->counters);
+        delete e;
+        return fail(HG_E_HIP, std::string(what) + ": " + hipGetErrorString(err));
+    };
+    hipError_t err;
+    if ((err = hipMalloc(&e->hmap, sizeof(float2) * rows * cols)) != hipSuccess) return cleanup(err, "hipMalloc terrain");
+    if ((err = hipMalloc(&e->state, sizeof(float) * kStateCols * num_envs)) != hipSuccess) return cleanup(err, "hipMalloc state");
+    if ((err = hipMalloc(&e->counters, sizeof(int32_t) * kCtrCols * num_envs)) != hipSuccess) return cleanup(err, "hipMalloc counters");
+    if ((err = hipMemcpy(e->hmap, e->hmap_host.data(), sizeof(float2) * rows * cols, hipMemcpyHostToDevice)) != hipSuccess)
+        return cleanup(err, "hipMemcpy terrain");
+    hipLaunchKernelGGL(init_kernel, dim3(grid_for(num_envs)), dim3(kBlock), 0, 0, e->tmpl, e->state, e->counters, num_envs);
+    if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "init_kernel");
+    if ((err = hipDeviceSynchronize()) != hipSuccess) return cleanup(err, "init sync");
+    *out = e;
+    return HG_OK;
+}
+
+void hg_destroy(hg_env* e) {
+    if (!e) return;
+    hipFree(e->hmap);
+    hipFree(e->state);
+    hipFree(e->counters);
+    delete e;
+}
+
+int64_t hg_num_envs(const hg_env* e) { return e ? e->n : -1; }
+
+int32_t hg_set_max_time(hg_env* e, double max_time) {
+    if (!e || !(max_time > 0)) return fail(HG_E_INVALID, "bad env or max_time");
+    e->cfg.max_time = max_time;
+    e->Pd = derive<double>(e->cfg, e->rows, e->cols);
+    e->Pf = derive<float>(e->cfg, e->rows, e->cols);
+    return HG_OK;
+}
+
+int32_t hg_set_target(hg_env* e, const hg_target* t) {
+    if (!e || !t) return fail(HG_E_INVALID, "bad env or target");
+    e->cfg.target = *t;
+    e->Pd = derive<double>(e->cfg, e->rows, e->cols);
+    e->Pf = derive<float>(e->cfg, e->rows, e->cols);
+    return HG_OK;
+}
+
+int32_t hg_set_trim_cond(hg_env* e, const hg_trim_cond* tc) {
+    if (!e || !tc) return fail(HG_E_INVALID, "bad env or trim cond");
+    const hg_trim_cond old = e->cfg.trim;
+    e->cfg.trim = *tc;
+    const int32_t rc = build_template(e);
+    if (rc != HG_OK) { e->cfg.trim = old; return rc; }
+    return HG_OK;
+}
+
+int32_t hg_get_template(const hg_env* e, hg_trim_result* out) {
+    if (!e || !out) return fail(HG_E_INVALID, "bad env or out");
+    *out = e->trim;
+    return HG_OK;
+}
+
+int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    hipLaunchKernelGGL(reset_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->tmpl,
+                       e->state, e->counters, mask, obs, e->n);
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count, int32_t* reset_index,
+                float* final_obs, void* stream) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    if (!actions || !obs || !reward || !terminated || !truncated)
+        return fail(HG_E_INVALID, "actions/obs/reward/terminated/truncated must be device pointers");
+    if (((uintptr_t)actions & 15) || ((uintptr_t)obs & 15))
+        return fail(HG_E_INVALID, "actions and obs must be 16-byte aligned");
+    if ((reset_index || final_obs) && !reset_count)
+        return fail(HG_E_INVALID, "reset_index/final_obs need reset_count");
+    hipStream_t s = (hipStream_t)stream;
+    if (reset_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
+    StepArgs a;
+    a.state = e->state;
+    a.counters = e->counters;
+    a.hmap = e->hmap;
+    a.actions = actions;
+    a.obs = obs;
+    a.reward = reward;
+    a.terminated = terminated;
+    a.truncated = truncated;
+    a.info = info;
+    a.eta = eta;
+    a.reset_count = reset_count;
+    a.reset_index = reset_index;
+    a.final_obs = final_obs;
+    a.n = e->n;
+    a.seed = e->cfg.seed;
+    a.env_offset = e->cfg.env_offset;
+    const dim3 grid(grid_for(e->n)), block(kBlock);
+    switch (e->cfg.task) {
+        case HG_TASK_HOVER:
+            hipLaunchKernelGGL(step_kernel<HG_TASK_HOVER>, grid, block, 0, s, e->Pf, e->tmpl, a);
+            break;
+        case HG_TASK_FORWARD_FLIGHT:
+            hipLaunchKernelGGL(step_kernel<HG_TASK_FORWARD_FLIGHT>, grid, block, 0, s, e->Pf, e->tmpl, a);
+            break;
+        default:
+            hipLaunchKernelGGL(step_kernel<HG_TASK_HELI>, grid, block, 0, s, e->Pf, e->tmpl, a);
+            break;
+    }
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    if (state) hipLaunchKernelGGL(soa_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->state, state, kStateCols, e->n);
+    if (counters)
+        hipLaunchKernelGGL(isoa_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->counters, counters, kCtrCols, e->n);
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, void* stream) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    hipStream_t s = (hipStream_t)stream;
+    if (state) hipLaunchKernelGGL(rows_to_soa, dim3(grid_for(e->n)), dim3(kBlock), 0, s, state, e->state, kStateCols, e->n);
+    if (counters)
+        hipLaunchKernelGGL(irows_to_soa, dim3(grid_for(e->n)), dim3(kBlock), 0, s, counters, e->counters, kCtrCols, e->n);
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_random_actions(hg_env* e, float* actions, uint64_t seed, uint64_t step, float lo, float hi, void* stream) {
+    if (!e || !actions) return fail(HG_E_INVALID, "env/actions is NULL");
+    if ((uintptr_t)actions & 15) return fail(HG_E_INVALID, "actions must be 16-byte aligned");
+    hipLaunchKernelGGL(random_actions_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream, actions,
+                       e->n, e->cfg.env_offset, seed, step, lo, hi);
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+}  // extern "C"

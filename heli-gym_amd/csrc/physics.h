@@ -1,0 +1,535 @@
+// physics.h — Heffley–Mnich minimum-complexity helicopter model + Dryden turbulence, written once
+// as __host__ __device__ templates: instantiated with float in the gfx950 step kernel
+// (heligym_amd.hip) and with double in the host trim (trim.h).
+//
+// Each function cites the reference code it re-states (paths relative to
+// /root/reference/heligym/envs/).  Quirks of the reference are kept on purpose and marked QUIRK.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#define HD __host__ __device__ __forceinline__
+
+namespace hg {
+
+// ------------------------------------------------------------------------------------------
+// math helpers: one overload per precision.  fp32 device versions use the hardware
+// transcendental units (v_log_f32 / v_exp_f32 / v_sqrt_f32).
+HD float m_sqrt(float x) { return sqrtf(x); }
+HD double m_sqrt(double x) { return sqrt(x); }
+HD float m_fabs(float x) { return fabsf(x); }
+HD double m_fabs(double x) { return fabs(x); }
+HD float m_floor(float x) { return floorf(x); }
+HD double m_floor(double x) { return floor(x); }
+HD float m_fmod(float x, float y) { return fmodf(x, y); }
+HD double m_fmod(double x, double y) { return fmod(x, y); }
+HD void m_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+HD void m_sincos(double x, double* s, double* c) { *s = sin(x); *c = cos(x); }
+// x^e for x > 0 (ISA density ratio, Dryden scale lengths)
+HD float m_pow(float x, float e) { return exp2f(e * log2f(x)); }
+HD double m_pow(double x, double e) { return pow(x, e); }
+HD float m_log2(float x) { return log2f(x); }
+HD double m_log2(double x) { return log2(x); }
+HD float m_exp2(float x) { return exp2f(x); }
+HD double m_exp2(double x) { return exp2(x); }
+template <typename R> HD R m_sign(R x) { return (R)((x > (R)0) - (x < (R)0)); }
+template <typename R> HD R m_max(R a, R b) { return a > b ? a : b; }
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kEps = 1e-4;                  // helicopter_dynamics.py:15, wind_dynamics.py:10
+constexpr double kSqrt3 = 1.7320508075688772;  // wind_dynamics.py:12
+constexpr double kTwoDPi = 0.6366197723675814; // wind_dynamics.py:13
+
+// ------------------------------------------------------------------------------------------
+// Derived model constants (helicopter_dynamics.py:107-154, wind_dynamics.py:21-37,
+// helicopter.py:63-68).  Computed once on the host in double (model.cpp) and cast to R.
+// Passed to the kernel by value, so every constant is a scalar (SGPR) operand.
+template <typename R>
+struct Params {
+    R dt, half_dt, dt6;
+    // control mixing u = c0 + c1 * action (helicopter_dynamics.py:414-422)
+    R coll0, coll1, lon0, lon1, lat0, lat1, ped0, ped1;
+    // ISA atmosphere rho = RO_SEA * (1 - LAPSE/T0 * alt)^rho_exp (:160-165)
+    R lapse_t0, ro_sea, rho_exp;
+    R wt, inv_mass, p_loss, vtrans, wl_cg_ft;
+    // main rotor
+    R mr_H, mr_D, mr_IS, mr_K1, mr_R, mr_OMEGA, mr_inv_OMEGA, mr_VTIP, mr_inv_VTIP;
+    R mr_tw75, mr_tw50, mr_two3_vtip, mr_gam_dro, mr_kc_num, mr_DL_DB1, mr_DL_DA1_dro, mr_coef;
+    R mr_inflow, mr_inv_thr_den, mr_inv_ct_den, mr_prof, mr_vtip2, mr_2_vtip, mr_8_asig;
+    // tail rotor
+    R tr_H, tr_D, tr_OMEGA, tr_VTIP, tr_inv_VTIP, tr_tw75, tr_tw50, tr_two3_vtip, tr_coef;
+    R tr_inflow, tr_inv_thr_den;
+    // fuselage
+    R fus_H, fus_XUU, fus_YVV, fus_ZWW, fus_COR, fus_dfw_k, fus_dfw_c;
+    // horizontal / vertical tail, wing
+    R ht_D, ht_ZUU, ht_ZUW, ht_ZMAX, ht_dw_k, ht_dw_c;
+    R vt_H, vt_D, vt_YUU, vt_YUV, vt_YMAX;
+    R wn_ZUU, wn_ZUW, wn_ZMAX;
+    int32_t wn_on;
+    // landing gear
+    R lg_K, lg_C, lg_loc[3][3];
+    // inertia: I = [[Ixx,0,Ixz],[0,Iyy,0],[Ixz,0,Izz]] (Ixz = -IXZ), and its inverse
+    R Ixx, Iyy, Izz, Ixz, Ji00, Ji02, Ji11, Ji20, Ji22;
+    // terrain (helicopter_dynamics.py:167-195)
+    R hm_sx, hm_sy, hm_cx, hm_cy, ns_half, ew_half;
+    int32_t hm_rows, hm_cols;
+    // Dryden wind (wind_dynamics.py:21-83)
+    R wm[3], wind_dir_cos, wind_dir_sin, w20, sigma_low, turb_level, eta_norm;
+    // task (helicopter.py:63-68, helicopter_with_tasks.py)
+    R n_t, n_t2, inv_n_x, inv_n_v, inv_n_a, tgt_n[3], vel_tgt_n, dwn_tgt_n;
+    R fail_zdot, fail_ang;
+    int32_t task, time_up_steps, success_steps, autoreset;
+};
+
+// Reset template: trimmed heli state, zero turbulence state, carry and observation.
+template <typename R>
+struct Template {
+    R heli[18];
+    R carry[4];
+    R obs[17];
+};
+
+template <typename R>
+struct Controls {
+    R coll, lon, lat, ped;
+};
+
+// helicopter_dynamics.py:414-422 (no clipping of the action, like the reference).
+template <typename R>
+HD Controls<R> controls(const Params<R>& P, R a0, R a1, R a2, R a3) {
+    Controls<R> u;
+    u.coll = P.coll0 + P.coll1 * a0;
+    u.lon = P.lon0 + P.lon1 * a1;
+    u.lat = P.lat0 + P.lat1 * a2;
+    u.ped = P.ped0 + P.ped1 * a3;
+    return u;
+}
+
+// utils.py:3-4 — floor-mod wrap to [-pi, pi).
+template <typename R>
+HD R pi_bound(R x) {
+    const R twopi = (R)(2 * kPi);
+    R r = m_fmod(x + (R)kPi, twopi);
+    r = r < (R)0 ? r + twopi : r;
+    return r - (R)kPi;
+}
+
+// helicopter_dynamics.py:167-195.  Three-point interpolated ground height at the COMMITTED (x, y).
+// The reference's scheme is discontinuous across cell edges, and the map centre (x = y = 0, where
+// every default trim starts) sits exactly on one; so the cell index must be decided exactly as the
+// fp64 reference decides it.  With an integer centre c, floor(x*s + c) = c + floor(x*s) exactly,
+// so the index comes from floor(x*s) (its sign is exact) instead of an fp32 x*s + c that rounds
+// to c for |x| below ~1e-4 ft.  Indices are clamped as integers as well, so a non-finite position
+// can never address outside the map.
+template <typename R>
+HD void map_coord(R t, int c, int hi, int* idx, R* frac) {
+    // x_loc = t + c clamped to [0, hi] (hi = rows - 1) -> (index, fraction) with x_loc = index + fraction
+    if (!(t > (R)(-c))) {            // x_loc <= 0 (and NaN) -> 0
+        *idx = 0;
+        *frac = (R)0;
+    } else if (t >= (R)(hi - c)) {   // x_loc >= hi -> hi
+        *idx = hi;
+        *frac = (R)0;
+    } else {
+        const R fl = m_floor(t);
+        *idx = (int)fl + c;
+        *frac = t - fl;
+    }
+}
+
+// Terrain texel = float2 {hi, lo} with hi + lo = the fp64 height (ft): the contact spring
+// K * (pos_z + h) and the ground altitude need h to better than one fp32 ulp of ~1500 ft.
+template <typename R>
+struct Ground {
+    R hi, lo, delta;   // h = (hi + lo) + delta; hi = the texel read before the edge decrement
+    HD R h() const { return (hi + lo) + delta; }
+    // z + h with the large cancellation done first (exact in fp32: Sterbenz lemma)
+    HD R zh(R z) const { return ((z + hi) + lo) + delta; }
+};
+
+template <typename R>
+HD Ground<R> ground_height(const Params<R>& P, const float2* __restrict__ hmap, R x, R y) {
+    const int rows = P.hm_rows, cols = P.hm_cols;
+    int xi, yi;
+    R fx, fy;
+    map_coord(x * P.hm_sx, rows / 2, rows - 1, &xi, &fx);
+    map_coord(y * P.hm_sy, cols / 2, rows - 1, &yi, &fy);   // QUIRK: y clamps to shape[0] (:182-183)
+    const float2 m = hmap[yi * cols + xi];   // read before the edge decrement (:188)
+    if (xi == rows - 1) { xi = rows - 2; fx += (R)1; }   // (:189-190,194) fractions use the
+    if (yi == cols - 1) { yi = cols - 2; fy += (R)1; }   // decremented index
+    const float2 n = hmap[yi * cols + xi + 1];
+    const float2 e = hmap[(yi + 1) * cols + xi];
+    Ground<R> g;
+    g.hi = (R)m.x;
+    g.lo = (R)m.y;
+    const R dn = ((R)n.x - (R)m.x) + ((R)n.y - (R)m.y);
+    const R de = ((R)e.x - (R)m.x) + ((R)e.y - (R)m.y);
+    g.delta = dn * fx + de * fy;
+    return g;
+}
+
+// ------------------------------------------------------------------------------------------
+// Dryden turbulence (wind_dynamics.py:54-125)
+
+template <typename R>
+struct WindPar {
+    R a_u, a_v, b_v, a_w, b_w;   // 1/t_u, 1/t_v, 1/(4 t_v^2), 1/t_w, 1/(4 t_w^2)
+    R K_u, K_v, K_w;             // sigma * sqrt(2/pi * t)
+    R cos_az, sin_az;
+};
+
+// lookup.py:146-183 (get_value_2D) on the 7x12 TEP table: row key = turbulence level, column
+// key = ground altitude; clamped linear interpolation, no extrapolation.
+// MIL-HDBK-1797 turbulence exceedance table as the reference fills its LookUpTable(7,12)
+// (wind_dynamics.py:29-37): row 0 = altitude keys, column 0 = level keys.
+#define HG_TEP_TABLE                                                                              \
+    {{0.f, 500.f, 1750.f, 3750.f, 7500.f, 15000.f, 25000.f, 35000.f, 45000.f, 55000.f, 65000.f,   \
+      75000.f, 80000.f},                                                                          \
+     {1.f, 3.2f, 2.2f, 1.5f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f},                        \
+     {2.f, 4.2f, 3.6f, 3.3f, 1.6f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f},                       \
+     {3.f, 6.6f, 6.9f, 7.4f, 6.7f, 4.6f, 2.7f, 0.4f, 0.f, 0.f, 0.f, 0.f, 0.f},                    \
+     {4.f, 8.6f, 9.6f, 10.6f, 10.1f, 8.0f, 6.6f, 5.0f, 4.2f, 2.7f, 0.f, 0.f, 0.f},                \
+     {5.f, 11.8f, 13.0f, 16.0f, 15.1f, 11.6f, 9.7f, 8.1f, 8.2f, 7.9f, 4.9f, 3.2f, 2.1f},          \
+     {6.f, 15.6f, 17.6f, 23.0f, 23.6f, 22.1f, 20.0f, 16.0f, 15.1f, 12.1f, 7.9f, 6.2f, 5.1f},      \
+     {7.f, 18.7f, 21.5f, 28.4f, 30.2f, 30.7f, 31.0f, 25.2f, 23.1f, 17.5f, 10.7f, 8.4f, 7.2f}}
+
+// lookup.py:146-183 (get_value_2D) on the 7x12 TEP table: row key = turbulence level, column
+// key = ground altitude; clamped linear interpolation, no extrapolation.  The reference caches
+// the last bracket index, which only changes where its search starts, not the bracket found.
+template <typename R>
+HD R tep_lookup(const float (*tep)[13], R rowKey, R colKey) {
+    int r = 2, c = 2;
+    for (int k = 0; k < 5; ++k) r += (r < 7 && (R)tep[r][0] < rowKey) ? 1 : 0;
+    for (int k = 0; k < 10; ++k) c += (c < 12 && (R)tep[0][c] < colKey) ? 1 : 0;
+    const R r0 = (R)tep[r - 1][0], r1 = (R)tep[r][0], k0 = (R)tep[0][c - 1], k1 = (R)tep[0][c];
+    R rF = (rowKey - r0) / (r1 - r0);
+    R cF = (colKey - k0) / (k1 - k0);
+    rF = rF > (R)1 ? (R)1 : (rF < (R)0 ? (R)0 : rF);
+    cF = cF > (R)1 ? (R)1 : (cF < (R)0 ? (R)0 : cF);
+    const R a0 = (R)tep[r - 1][c - 1], a1 = (R)tep[r][c - 1], b0 = (R)tep[r - 1][c], b1 = (R)tep[r][c];
+    const R c1 = rF * (a1 - a0) + a0;
+    const R c2 = rF * (b1 - b0) + b0;
+    return c1 + cF * (c2 - c1);
+}
+
+// wind_dynamics.py:54-83 (_calc_params) folded with the stage-invariant part of :92-99, 112-118.
+template <typename R>
+HD WindPar<R> wind_params(const Params<R>& P, const float (*tep)[13], const R carry[4]) {
+    const R vx = carry[0] + P.wm[0], vy = carry[1] + P.wm[1], vz = carry[2] + P.wm[2];
+    const R vel = m_sqrt(vx * vx + vy * vy + vz * vz);
+    R h = carry[3];
+    R Lu, Lv, Lw, s_u, s_v, s_w, ca, sa;
+    if (h <= (R)1000) {                       // low altitude
+        h = m_max(h, (R)10);
+        const R lb = m_log2((R)0.177 + (R)0.000823 * h);
+        Lu = h * m_exp2((R)-1.2 * lb);
+        Lv = (R)0.5 * Lu;
+        Lw = (R)0.5 * h;
+        s_w = P.sigma_low;
+        s_u = s_w * m_exp2((R)-0.4 * lb);
+        s_v = s_u;
+        ca = P.wind_dir_cos;
+        sa = P.wind_dir_sin;
+    } else {
+        R ax, ay;
+        if (h >= (R)2000) {                   // high altitude
+            Lu = (R)1750; Lv = (R)875; Lw = (R)875;
+            s_u = tep_lookup(tep, P.turb_level, h);
+            ax = vx; ay = vy;
+        } else {                              // medium: blend of the two (QUIRK: Lw = Lu, :76)
+            const R r = (h - (R)1000) * (R)0.001;
+            Lu = (R)1000 + r * (R)750;
+            Lv = (R)0.5 * Lu;
+            Lw = Lu;
+            s_u = P.sigma_low + r * (tep_lookup(tep, P.turb_level, h) - P.sigma_low);
+            ax = vx * r + P.wm[0] * ((R)1 - r);
+            ay = vy * r + P.wm[1] * ((R)1 - r);
+        }
+        s_v = s_u; s_w = s_u;
+        // cos/sin of atan2(ay, ax) without the transcendental (atan2(0,0) = 0)
+        const R hyp = m_sqrt(ax * ax + ay * ay);
+        const bool z = !(hyp > (R)0);
+        const R ih = z ? (R)0 : (R)1 / hyp;
+        ca = z ? (R)1 : ax * ih;
+        sa = z ? (R)0 : ay * ih;
+    }
+    const R iv = (R)1 / (vel + (R)kEps);
+    const R t_u = Lu * iv, t_v = Lv * iv, t_w = Lw * iv;
+    WindPar<R> w;
+    w.a_u = (R)1 / t_u;
+    w.a_v = (R)1 / t_v;
+    w.b_v = (R)0.25 * w.a_v * w.a_v;
+    w.a_w = (R)1 / t_w;
+    w.b_w = (R)0.25 * w.a_w * w.a_w;
+    w.K_u = s_u * m_sqrt((R)kTwoDPi * t_u);
+    w.K_v = s_v * m_sqrt((R)kTwoDPi * t_v);
+    w.K_w = s_w * m_sqrt((R)kTwoDPi * t_w);
+    w.cos_az = ca;
+    w.sin_az = sa;
+    return w;
+}
+
+// wind_dynamics.py:101-109
+template <typename R>
+HD void wind_f(const WindPar<R>& w, const R eta[3], const R s[5], R d[5]) {
+    d[0] = w.a_u * (eta[0] - s[0]);
+    d[1] = w.b_v * (eta[1] - s[2]) - w.a_v * s[1];
+    d[2] = s[1];
+    d[3] = w.b_w * (eta[2] - s[4]) - w.a_w * s[3];
+    d[4] = s[3];
+}
+
+// WindDynamics.step (dynamics.py:158-171 + wind_dynamics.py:85-125).  QUIRK: the
+// derivative object is aliased across the RK stages, so the update is s += dt * k4; the stage
+// inputs are still formed from k1..k3.  Wind output from the stage-4 input state.
+template <typename R>
+HD void wind_step(const Params<R>& P, const float (*tep)[13], R s[5], const R carry[4], const R eta[3],
+                  R W[3]) {
+    const WindPar<R> w = wind_params(P, tep, carry);
+    R k[5], st[5];
+    wind_f(w, eta, s, k);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) st[i] = s[i] + k[i] * P.half_dt;
+    wind_f(w, eta, st, k);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) st[i] = s[i] + k[i] * P.half_dt;
+    wind_f(w, eta, st, k);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) st[i] = s[i] + k[i] * P.dt;
+    wind_f(w, eta, st, k);
+    const R ut = w.K_u * st[0];
+    const R vt = w.K_v * (st[2] + (R)(2 * kSqrt3) * st[1]);
+    const R wt = w.K_w * (st[4] + (R)(2 * kSqrt3) * st[3]);
+    W[0] = P.wm[0] + (w.cos_az * ut - w.sin_az * vt);
+    W[1] = P.wm[1] + (w.sin_az * ut + w.cos_az * vt);
+    W[2] = P.wm[2] + wt;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) s[i] = s[i] + P.dt * k[i];
+}
+
+// ------------------------------------------------------------------------------------------
+// HelicopterDynamics.dynamics (helicopter_dynamics.py:400-489).
+// s: [vi_mr vi_tr psi_mr psi_tr b0 b1 u v w p q r phi theta psi x y z]; W: wind NED; h_c: ground
+// height under the COMMITTED position (F6).  Writes d[18]; with OBS also the 17 observations.
+template <bool OBS, typename R>
+HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>& u, const R W[3],
+                 const Ground<R>& gc, R* __restrict__ d, R* __restrict__ obs) {
+    const R vi_mr = s[0], vi_tr = s[1], b0 = s[4], b1 = s[5];
+    const R uu = s[6], vv = s[7], ww = s[8], p = s[9], q = s[10], r = s[11];
+    const R phi = s[12], th = s[13], psi = s[14];
+    const R z = s[17];
+
+    // kinematic.py:3-29: B = earth->body DCM, T = pqr->euler rate
+    R s0, c0, s1, c1, s2, c2;
+    m_sincos(phi, &s0, &c0);
+    m_sincos(th, &s1, &c1);
+    m_sincos(psi, &s2, &c2);
+    const R B00 = c1 * c2, B01 = c1 * s2, B02 = -s1;
+    const R s0s1 = s0 * s1, c0s1 = c0 * s1;
+    const R B10 = s0s1 * c2 - c0 * s2, B11 = s0s1 * s2 + c0 * c2, B12 = s0 * c1;
+    const R B20 = c0s1 * c2 + s0 * s2, B21 = c0s1 * s2 - s0 * c2, B22 = c0 * c1;
+    const R ic1 = (R)1 / c1;
+    const R t1 = s1 * ic1;
+    const R phid = p + (s0 * t1) * q + (c0 * t1) * r;
+    const R thd = c0 * q - s0 * r;
+    const R psid = (s0 * ic1) * q + (c0 * ic1) * r;
+    // ned = B^T uvw, uvw_air = uvw - B W (:428-431)
+    const R n0 = B00 * uu + B10 * vv + B20 * ww;
+    const R n1 = B01 * uu + B11 * vv + B21 * ww;
+    const R n2 = B02 * uu + B12 * vv + B22 * ww;
+    const R ua = uu - (B00 * W[0] + B01 * W[1] + B02 * W[2]);
+    const R va = vv - (B10 * W[0] + B11 * W[1] + B12 * W[2]);
+    const R wa = ww - (B20 * W[0] + B21 * W[1] + B22 * W[2]);
+    const R power_climb = P.wt * (-n2);
+    // ISA density at altitude -z (:160-165)
+    const R rho = P.ro_sea * m_pow((R)1 + P.lapse_t0 * z, P.rho_exp);
+
+    // ---- main rotor (:203-270)
+    const R gam = rho * P.mr_gam_dro;
+    const R igam = (R)1 / gam;
+    const R KC = P.mr_kc_num * igam + P.mr_K1;
+    const R og = P.mr_OMEGA * igam;
+    const R ITB2_OM = P.mr_OMEGA / ((R)1 + og * og);
+    const R ITB = ITB2_OM * og;
+    const R DL_DA1 = rho * P.mr_DL_DA1_dro;
+    const R vadv2 = ua * ua + va * va;
+    const R wr = wa + (b0 - P.mr_IS) * ua - b1 * va;
+    const R wb = wr + P.mr_two3_vtip * (u.coll + P.mr_tw75) + vadv2 * P.mr_inv_VTIP * (u.coll + P.mr_tw50);
+    const R thr = (wb - vi_mr) * rho * P.mr_coef;
+    const R irho = (R)1 / rho;
+    const R dw = wr - vi_mr;
+    d[0] = P.mr_inflow * (thr * irho * P.mr_inv_thr_den - vi_mr * m_sqrt(vadv2 + dw * dw));
+    const R power_mr = thr * (vi_mr - wr) + rho * P.mr_prof * (P.mr_vtip2 + (R)3 * vadv2);
+    R CT = thr * irho * P.mr_inv_ct_den;
+    CT = CT > (R)0 ? CT : (R)0;
+    const R DB1DV = P.mr_2_vtip * (P.mr_8_asig * CT + m_sqrt((R)0.5 * CT));
+    const R wake = m_fabs(ua) > P.vtrans ? (R)1 : (R)0;
+    const R a_sum = b1 - u.lat + KC * b0 + DB1DV * va * ((R)1 + wake);
+    const R b_sum = b0 + u.lon - KC * b1 - DB1DV * ua * ((R)1 + (R)2 * wake);
+    d[4] = -ITB * b_sum - ITB2_OM * a_sum - q;
+    d[5] = -ITB * a_sum + ITB2_OM * b_sum - p;
+    d[2] = P.mr_OMEGA;
+    const R X_MR = -thr * (b0 - P.mr_IS), Y_MR = thr * b1, Z_MR = -thr;
+    const R L_MR = Y_MR * P.mr_H + P.mr_DL_DB1 * b1 + DL_DA1 * (b0 + u.lon - P.mr_K1 * b1);
+    const R M_MR = Z_MR * P.mr_D - X_MR * P.mr_H + P.mr_DL_DB1 * b0 + DL_DA1 * (-b1 + u.lat - P.mr_K1 * b0);
+
+    // ---- tail rotor (:272-300)
+    const R wq = wa + q * P.tr_D;
+    const R vadv2t = wq * wq + ua * ua;
+    const R vr = -(va - r * P.tr_D + p * P.tr_H);
+    const R vb = vr + P.tr_two3_vtip * (u.ped + P.tr_tw75) + vadv2t * P.tr_inv_VTIP * (u.ped + P.tr_tw50);
+    const R thr_t = (vb - vi_tr) * rho * P.tr_coef;
+    const R dwt = vr - vi_tr;
+    d[1] = P.tr_inflow * (thr_t * irho * P.tr_inv_thr_den - vi_tr * m_sqrt(vadv2t + dwt * dwt));
+    d[3] = P.tr_OMEGA;
+    const R power_tr = thr_t * (vi_tr - vr);
+
+    // ---- fuselage (:302-320)
+    R wa_f = wa - vi_mr;
+    wa_f = wa_f > (R)0 ? wa_f + (R)kEps : wa_f;
+    const R d_fw = ((ua / (-wa_f)) * P.fus_dfw_k - P.fus_dfw_c) * P.fus_COR;
+    const R rh = (R)0.5 * rho;
+    const R X_F = rh * P.fus_XUU * m_fabs(ua) * ua;
+    const R Y_F = rh * P.fus_YVV * m_fabs(va) * va;
+    const R Z_F = rh * P.fus_ZWW * m_fabs(wa_f) * wa_f;
+    const R power_fus = -X_F * ua - Y_F * va - Z_F * wa_f;
+
+    // ---- horizontal tail (:322-345)
+    const R v_dw = m_max(vi_mr - wa, (R)kEps);
+    const R d_dw = ua / v_dw * P.ht_dw_k - P.ht_dw_c;
+    const R eps_ht = (d_dw > (R)0 && d_dw < P.mr_R) ? (R)2 * ((R)1 - d_dw / P.mr_R) : (R)0;
+    const R wa_ht = wa - eps_ht * vi_mr + P.ht_D * q;
+    const R aua = m_fabs(ua);
+    R Z_HT;
+    if (m_fabs(wa_ht) > (R)0.3 * aua)
+        Z_HT = rh * P.ht_ZMAX * m_sqrt(ua * ua + va * va + wa_ht * wa_ht) * wa_ht;
+    else
+        Z_HT = rh * (P.ht_ZUU * aua * ua + P.ht_ZUW * aua * wa_ht);
+
+    // ---- vertical tail (:347-361)
+    const R va_vt = va + vi_tr - P.vt_D * r;
+    R Y_VT;
+    if (m_fabs(va_vt) > (R)0.3 * aua)
+        Y_VT = rh * P.vt_YMAX * m_sqrt(ua * ua + va_vt * va_vt) * va_vt;
+    else
+        Y_VT = rh * (P.vt_YUU * aua * ua + P.vt_YUV * aua * va_vt);
+
+    // ---- wing (:363-383); the AW109 has none (ZUW = 0), the branch is uniform
+    R X_WN = (R)0, Z_WN = (R)0;
+    if (P.wn_on) {
+        const R wa_w = wa - vi_mr;
+        const R vta2 = ua * ua + wa_w * wa_w;
+        const R qq = P.wn_ZUU * ua * ua + P.wn_ZUW * ua * wa_w;
+        Z_WN = m_fabs(wa_w) > (R)0.3 * aua ? rh * P.wn_ZMAX * m_sqrt(vta2) * wa_w : rh * qq;
+        X_WN = -rh / (R)kPi / vta2 * qq * qq;
+    }
+    const R power_wn = m_fabs(X_WN * ua);
+
+    // ---- landing gear (:385-398).  QUIRK: the moment uses the ACCUMULATED force (:397).
+    // z + h is formed with the cancellation first (Ground::zh), so the stiff spring force
+    // K * (pos_z + h) keeps its precision near the ground.
+    R Fl0 = 0, Fl1 = 0, Fl2 = 0, Ml0 = 0, Ml1 = 0, Ml2 = 0;
+    const R zh = gc.zh(z);
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        const R rx = P.lg_loc[g][0], ry = P.lg_loc[g][1], rz = P.lg_loc[g][2];
+        const R pzh = zh + (B02 * rx + B12 * ry + B22 * rz);   // pos_z + h
+        if (-pzh - P.wl_cg_ft < (R)0) {                        // -pos_z - (h + WL_CG/12) < 0
+            const R cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
+            const R vel_z = n2 + (B02 * cx + B12 * cy + B22 * cz);
+            const R fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (R)kEps;
+            Fl0 += B02 * fz; Fl1 += B12 * fz; Fl2 += B22 * fz;
+            Ml0 += ry * Fl2 - rz * Fl1;
+            Ml1 += rz * Fl0 - rx * Fl2;
+            Ml2 += rx * Fl1 - ry * Fl0;
+        }
+    }
+
+    // ---- totals and rigid-body EOM (:446-470)
+    const R p_extra = power_climb + power_fus;
+    const R Fx = X_MR + X_F + X_WN + P.wt * B02 + Fl0;
+    const R Fy = Y_MR + thr_t + Y_F + Y_VT + P.wt * B12 + Fl1;
+    const R Fz = Z_MR + Z_F + Z_HT + Z_WN + P.wt * B22 + Fl2;
+    const R Mx = L_MR + thr_t * P.tr_H + Y_F * P.fus_H + Y_VT * P.vt_H + Ml0;
+    const R My = M_MR + (Z_F * d_fw - X_F * P.fus_H) + Z_HT * P.ht_D + Ml1;
+    const R Mz = (power_mr * P.mr_inv_OMEGA + p_extra * P.mr_inv_OMEGA) - thr_t * P.tr_D - Y_VT * P.vt_D + Ml2;
+    d[6] = Fx * P.inv_mass - (q * ww - r * vv);
+    d[7] = Fy * P.inv_mass - (r * uu - p * ww);
+    d[8] = Fz * P.inv_mass - (p * vv - q * uu);
+    const R Ip0 = P.Ixx * p + P.Ixz * r, Ip1 = P.Iyy * q, Ip2 = P.Ixz * p + P.Izz * r;
+    const R g0 = Mx - (q * Ip2 - r * Ip1);
+    const R g1 = My - (r * Ip0 - p * Ip2);
+    const R g2 = Mz - (p * Ip1 - q * Ip0);
+    d[9] = P.Ji00 * g0 + P.Ji02 * g2;
+    d[10] = P.Ji11 * g1;
+    d[11] = P.Ji20 * g0 + P.Ji22 * g2;
+    d[12] = phid; d[13] = thd; d[14] = psid;
+    d[15] = n0; d[16] = n1; d[17] = n2;
+    if (OBS) {   // :471-488 (observation at this stage's input state)
+        const R power_total = power_mr + power_tr + p_extra + power_wn + P.p_loss;
+        obs[0] = power_total * (R)(1.0 / 550.0);
+        obs[1] = ua; obs[2] = va; obs[3] = wa;
+        obs[4] = n0; obs[5] = n1; obs[6] = n2;
+        obs[7] = phi; obs[8] = th; obs[9] = psi;
+        obs[10] = p; obs[11] = q; obs[12] = r;
+        obs[13] = s[15]; obs[14] = s[16]; obs[15] = -z; obs[16] = -zh;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Tasks and flags
+
+// HeliHover._calculate_reward (helicopter_with_tasks.py:27-52)
+template <typename R>
+HD R reward_hover(const Params<R>& P, const R s[18], const R d[18], bool* success) {
+    R pf = 0, pt = 0, xf = 0, xt = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const R pn = s[9 + i] * P.n_t, pdn = d[9 + i] * P.n_t2;
+        const R e = s[15 + i] * P.inv_n_x - P.tgt_n[i];
+        pf -= pn * pn;
+        pt -= m_sign(pn) * pdn;
+        xf -= e * e;
+        xt -= m_sign(e) * (d[15 + i] * P.inv_n_v);
+    }
+    *success = pf > (R)-1 && xf > (R)-1;
+    return (m_max(pf, pt) + m_max(xf, xt)) * (R)0.5;
+}
+
+// HeliForwardFlight._calculate_reward (helicopter_with_tasks.py:78-115).  QUIRK: divides by the
+// speed, so a helicopter at exactly zero velocity gets a NaN reward like the reference.
+template <typename R>
+HD R reward_forward(const Params<R>& P, const R s[18], const R d[18], bool* success) {
+    const R vel = m_sqrt(s[6] * s[6] + s[7] * s[7] + s[8] * s[8]);
+    const R vn = vel * P.inv_n_v;
+    const R vdn = (s[6] * d[6] + s[7] * d[7] + s[8] * d[8]) / vel * P.inv_n_a;
+    const R dn = s[17] * P.inv_n_x, ddn = d[17] * P.inv_n_v;
+    R pf = 0, pt = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const R pn = s[9 + i] * P.n_t, pdn = d[9 + i] * P.n_t2;
+        pf -= pn * pn;
+        pt -= m_sign(pn) * pdn;
+    }
+    const R ev = vn - P.vel_tgt_n, ed = dn - P.dwn_tgt_n;
+    const R vf = -ev * ev, vt = -m_sign(ev) * vdn;
+    const R df = -ed * ed, dtt = -m_sign(ed) * ddn;
+    *success = pf > (R)-1 && vf > (R)-1 && df > (R)-1;
+    return (m_max(pf, pt) + m_max(vf, vt) + m_max(df, dtt)) * (R)(1.0 / 3.0);
+}
+
+// Heli._is_failed (helicopter.py:226-234) on the post-step state, k4 derivatives and the ground
+// height under the post-step position.
+template <typename R>
+HD bool is_failed(const Params<R>& P, const R s[18], const R d[18], const Ground<R>& gp) {
+    const R gta = gp.h() + P.wl_cg_ft;
+    const bool hit = -gp.zh(s[17]) - P.wl_cg_ft < (R)0;
+    const bool c2 = d[17] > P.fail_zdot;
+    const bool c3 = s[12] > P.fail_ang, c4 = s[13] > P.fail_ang;
+    const bool c5 = m_fabs(s[15]) > P.ns_half || m_fabs(s[16]) > P.ew_half || -s[17] > gta + (R)10000;
+    return (hit && (c2 || c3 || c4)) || c5;
+}
+
+}  // namespace hg

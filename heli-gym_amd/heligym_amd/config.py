@@ -48,8 +48,8 @@ def load_terrain(doc):
 
 
 def terrain_ft(u16, max_gr_alt):
-    """Heights in ft as float32 (the kernel's table); reference: png / 65535 * MAX_GR_ALT."""
-    return ((u16.astype(np.float64) / 65535.0) * max_gr_alt).astype(np.float32)
+    """Heights in ft, fp64 exactly as the reference computes them: png / 65535 * MAX_GR_ALT."""
+    return np.ascontiguousarray((u16.astype(np.float64) / 65535.0) * max_gr_alt)
 
 
 def fill_trim(tc, trim_cond):

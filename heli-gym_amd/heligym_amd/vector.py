@@ -1,0 +1,239 @@
+"""Batched heli-gym environment on one MI355X: N helicopters advanced by one HIP kernel per step.
+
+`HeliVecEnv` is the vectorised counterpart of the reference's `Heli` gymnasium env
+(heligym/envs/helicopter.py:28-243): same 17-observation / 4-action contract, same reward, flags and
+setters, with same-step auto-reset.  All buffers are PyTorch-ROCm tensors on the env's device; the
+step itself runs in `libheligym_amd.so` (no CPU path exists).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi, config
+
+
+class Box:
+    """Minimal stand-in for gymnasium.spaces.Box (gymnasium is optional)."""
+
+    def __init__(self, low, high, shape, dtype=np.float32):
+        self.low = np.full(shape, low, dtype=dtype)
+        self.high = np.full(shape, high, dtype=dtype)
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+
+    def sample(self, rng=np.random):
+        lo = np.where(np.isfinite(self.low), self.low, -1.0)
+        hi = np.where(np.isfinite(self.high), self.high, 1.0)
+        return rng.uniform(lo, hi).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+
+def _make_box(low, high, shape):
+    try:  # use the real class when gymnasium is installed
+        from gymnasium import spaces
+        return spaces.Box(low, high, shape=shape, dtype=np.float32)
+    except ImportError:
+        return Box(low, high, shape)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+OBS_NAMES = ("POWER", "LON_AIR_SPD", "LAT_AIR_SPD", "DWN_AIR_SPD", "N_VEL", "E_VEL", "DES_RATE",
+             "ROLL", "PITCH", "YAW", "ROLL_RATE", "PITCH_RATE", "YAW_RATE",
+             "N_POS", "E_POS", "ALTITUDE", "GROUND_ALTITUDE")   # helicopter_dynamics.py:23-25
+
+
+class HeliVecEnv:
+    """N independent helicopters (one `hg_env` handle) on one GPU.
+
+    task: "hover" (HeliHover), "forward_flight" (HeliForwardFlight) or "heli" (Heli, reward 0).
+    autoreset: finished envs are reset inside the step kernel; the returned observation row is
+      the reset observation and the terminal one is in info["final_obs"] (rows of
+      info["reset_index"]).  With autoreset=False, finished envs keep integrating until reset().
+    env_offset: global id of env 0 (multi-GPU sharding keeps the noise stream of each env fixed).
+    """
+
+    metadata = {"render.modes": [], "video.frames_per_second": config.FPS}   # helicopter.py:29-32
+
+    def __init__(self, num_envs, task="hover", dt=config.DT, heli_name="aw109", seed=0, device=None,
+                 autoreset=True, env_offset=0, max_time=None, target=None, trim_cond=None,
+                 turbulence_level=None):
+        import torch
+        self.torch = torch
+        self.lib = _abi.load_library()
+        if not torch.cuda.is_available():
+            raise _abi.HeliGymError("HeliVecEnv needs a HIP device (no CPU fallback)")
+        self.device = torch.device(device if device is not None else f"cuda:{torch.cuda.current_device()}")
+        self.num_envs = int(num_envs)
+        self.task = task
+        self.dt = float(dt)
+        self.autoreset = bool(autoreset)
+        self.cfg, doc = config.make_config(task=task, dt=dt, heli_name=heli_name, max_time=max_time,
+                                           target=target, trim_cond=trim_cond, autoreset=autoreset,
+                                           seed=seed, env_offset=env_offset,
+                                           turbulence_level=turbulence_level)
+        u16 = config.load_terrain(doc)
+        self.terrain_ft = config.terrain_ft(u16, self.cfg.af.env_MAX_GR_ALT)
+        self._target = dict(config.DEFAULT_TARGETS[task])
+        self._target.update(target or {})
+        self._trim_cond = config.fill_trim(_abi.hg_trim_cond(), trim_cond)
+        self.max_time = self.cfg.max_time
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.hg_create(ctypes.byref(self.cfg), self.terrain_ft.ctypes.data,
+                                          self.terrain_ft.shape[0], self.terrain_ft.shape[1],
+                                          self.num_envs, ctypes.byref(h)), self.lib)
+        self._h = h
+        N, dev = self.num_envs, self.device
+        f32, u8, i32 = torch.float32, torch.uint8, torch.int32
+        self.obs = torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)
+        self.reward = torch.empty((N,), dtype=f32, device=dev)
+        self.terminated_u8 = torch.empty((N,), dtype=u8, device=dev)
+        self.truncated_u8 = torch.empty((N,), dtype=u8, device=dev)
+        self.info_u8 = torch.empty((N,), dtype=u8, device=dev)
+        self.reset_count = torch.zeros((1,), dtype=i32, device=dev)
+        self.reset_index = torch.empty((N,), dtype=i32, device=dev)
+        self.final_obs = torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)
+        self.observation_space = _make_box(-np.inf, np.inf, (_abi.HG_N_OBS,))   # helicopter.py:56
+        self.action_space = _make_box(-1.0, 1.0, (_abi.HG_N_ACT,))              # helicopter.py:57
+        self.normalizers = {                                                     # helicopter.py:63-68
+            "t": float(np.sqrt(2 * self.cfg.af.mr_R / self.cfg.af.env_GRAV)),
+            "x": 2 * self.cfg.af.mr_R,
+            "v": float(np.sqrt(2 * self.cfg.af.mr_R * self.cfg.af.env_GRAV)),
+            "a": self.cfg.af.env_GRAV,
+        }
+
+    # ------------------------------------------------------------------ plumbing
+    def _stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _check(self, rc):
+        return _abi.check(rc, self.lib)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.hg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ gym surface
+    def reset(self, seed=None, options=None, mask=None):
+        """Heli.reset (helicopter.py:208-217) for all envs, or for the envs where `mask` != 0.
+        Returns (obs [N,17], info) like the reference (obs rows of unmasked envs untouched)."""
+        m = None
+        if mask is not None:
+            m = self.torch.as_tensor(mask, device=self.device).to(self.torch.uint8).contiguous()
+        self._check(self.lib.hg_reset(self._h, _ptr(m), _ptr(self.obs), self._stream()))
+        tr = self.template()
+        N = self.num_envs
+        info = {"failed": self.torch.full((N,), bool(tr["failed"]), device=self.device),
+                "successed": self.torch.zeros((N,), dtype=self.torch.bool, device=self.device),
+                "time_up": self.torch.zeros((N,), dtype=self.torch.bool, device=self.device)}
+        return self.obs, info
+
+    def step_async(self, actions, eta=None, with_reset_info=True):
+        """Launch one step on the current stream and return immediately (no host sync).
+        actions: float32 [N,4] device tensor.  eta: optional float32 [N,3] injected turbulence noise
+        (already scaled by 1/sqrt(dt)), else in-kernel Philox."""
+        a = actions
+        if a.dtype != self.torch.float32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=self.torch.float32).contiguous()
+        if tuple(a.shape) != (self.num_envs, _abi.HG_N_ACT):
+            raise ValueError(f"actions must be [{self.num_envs}, 4], got {tuple(a.shape)}")
+        e = None
+        if eta is not None:
+            e = eta.to(device=self.device, dtype=self.torch.float32).contiguous()
+            if tuple(e.shape) != (self.num_envs, 3):
+                raise ValueError("eta must be [N, 3]")
+        self._keep = (a, e)
+        rs = with_reset_info and self.autoreset
+        self._check(self.lib.hg_step(
+            self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated_u8),
+            _ptr(self.truncated_u8), _ptr(self.info_u8), _ptr(e),
+            _ptr(self.reset_count) if rs else None, _ptr(self.reset_index) if rs else None,
+            _ptr(self.final_obs) if rs else None, self._stream()))
+
+    def step(self, actions, eta=None):
+        """Heli.step (helicopter.py:192-206) for all envs: (obs, reward, terminated, truncated, info).
+        Returned tensors are the env's buffers, overwritten by the next step."""
+        self.step_async(actions, eta)
+        t = self.torch
+        bits = self.info_u8
+        info = {"failed": (bits & _abi.HG_INFO_FAILED) != 0,
+                "successed": (bits & _abi.HG_INFO_SUCCESSED) != 0,
+                "time_up": (bits & _abi.HG_INFO_TIME_UP) != 0,
+                "success_step": (bits & _abi.HG_INFO_SUCCESS_STEP) != 0}
+        if self.autoreset:
+            k = int(self.reset_count.item())
+            idx = self.reset_index[:k].long()
+            order = t.argsort(idx)
+            info["reset_index"] = idx[order]
+            info["final_obs"] = self.final_obs[:k][order]
+        return self.obs, self.reward, self.terminated_u8.bool(), self.truncated_u8.bool(), info
+
+    # ------------------------------------------------------------------ setters (helicopter.py:89-111)
+    def set_max_time(self, max_time=None):
+        self.max_time = config.DEFAULT_MAX_TIME if max_time is None else float(max_time)
+        self._check(self.lib.hg_set_max_time(self._h, self.max_time))
+
+    def set_target(self, target=None):
+        self._target.update(target or {})
+        tg = _abi.hg_target()
+        config.fill_target(tg, self._target)
+        self._check(self.lib.hg_set_target(self._h, ctypes.byref(tg)))
+
+    def get_target(self):
+        return dict(self._target)
+
+    def set_trim_cond(self, trim_cond=None):
+        cur = self.get_trim_cond()
+        cur.update(trim_cond or {})
+        tc = _abi.hg_trim_cond()
+        self._trim_cond = config.fill_trim(tc, cur)
+        self._check(self.lib.hg_set_trim_cond(self._h, ctypes.byref(tc)))
+
+    def get_trim_cond(self):
+        import copy
+        return copy.deepcopy(self._trim_cond)
+
+    def template(self):
+        r = _abi.hg_trim_result()
+        self._check(self.lib.hg_get_template(self._h, ctypes.byref(r)))
+        return {"state": np.array(r.state), "action": np.array(r.action), "obs": np.array(r.obs),
+                "state_dots": np.array(r.state_dots), "residual": r.residual,
+                "iterations": r.iterations, "failed": bool(r.failed)}
+
+    # ------------------------------------------------------------------ state access
+    def get_state(self):
+        """(state [N,27] float32, counters [N,3] int32): heli 18 | wind 5 | carry 4."""
+        t = self.torch
+        s = t.empty((self.num_envs, _abi.HG_STATE_COLS), dtype=t.float32, device=self.device)
+        c = t.empty((self.num_envs, _abi.HG_COUNTER_COLS), dtype=t.int32, device=self.device)
+        self._check(self.lib.hg_get_state(self._h, _ptr(s), _ptr(c), self._stream()))
+        return s, c
+
+    def set_state(self, state=None, counters=None):
+        t = self.torch
+        s = None if state is None else t.as_tensor(state, device=self.device, dtype=t.float32).contiguous()
+        c = None if counters is None else t.as_tensor(counters, device=self.device, dtype=t.int32).contiguous()
+        if s is not None and tuple(s.shape) != (self.num_envs, _abi.HG_STATE_COLS):
+            raise ValueError("state must be [N, 27]")
+        if c is not None and tuple(c.shape) != (self.num_envs, _abi.HG_COUNTER_COLS):
+            raise ValueError("counters must be [N, 3]")
+        self._check(self.lib.hg_set_state(self._h, _ptr(s), _ptr(c), self._stream()))
+        self._keep_state = (s, c)
+
+    def random_actions(self, out, seed, step, lo=-1.0, hi=1.0):
+        self._check(self.lib.hg_random_actions(self._h, _ptr(out), int(seed), int(step), float(lo),
+                                               float(hi), self._stream()))
+        return out

@@ -127,15 +127,16 @@ void hg_default_config(hg_config* cfg);
 /* Trim (host, fp64).  Replaces HelicopterDynamics.trim / __trim_fcn
  * (helicopter_dynamics.py:491-576) as called from reset (:66-71).  `terrain_ft` is the
  * [rows, cols] ground-height map in ft (helicopter_dynamics.py:39-43), `wind_ned` the wind the
- * trim is solved against (helicopter.py:55: the mean wind). */
-int32_t hg_trim(const hg_config* cfg, const float* terrain_ft, int32_t rows, int32_t cols,
+ * trim is solved against (helicopter.py:55: the mean wind).  Heights are fp64 like the reference's
+ * png/65535*MAX_GR_ALT; the library keeps each as an fp32 {hi, lo} pair. */
+int32_t hg_trim(const hg_config* cfg, const double* terrain_ft, int32_t rows, int32_t cols,
                 const double wind_ned[3], hg_trim_result* out);
 
 /* Handle lifetime: replaces Heli.__init__ (helicopter.py:47-86: yaml params, HelicopterDynamics
  * and WindDynamics construction, terrain load) for `num_envs` independent helicopters, and
  * Heli.close (helicopter.py:185-187).  Uploads the terrain, derives the model constants, trims
  * the reset template against the mean wind. */
-int32_t hg_create(const hg_config* cfg, const float* terrain_ft, int32_t rows, int32_t cols,
+int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, int32_t cols,
                   int64_t num_envs, hg_env** out);
 void hg_destroy(hg_env* env);
 int64_t hg_num_envs(const hg_env* env);

@@ -411,6 +411,14 @@ static void cross(const double a[3], const double b[3], double o[3]) {   /* util
     o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
+/* Diagnostics for the parity tests: the smallest |gear clearance| seen by the landing-gear contact
+ * test (helicopter_dynamics.py:393) since the last or_diag_reset().  The reference's contact force
+ * jumps by K * WL_CG/12 (~96 000 lb) when a gear crosses that threshold, so a step whose clearance
+ * is within rounding of 0 is ill-conditioned for any finite-precision comparison. */
+static __thread double g_lg_margin = INFINITY;
+void or_diag_reset(void) { g_lg_margin = INFINITY; }
+double or_diag_lg_margin(void) { return g_lg_margin; }
+
 /* HelicopterDynamics.dynamics (helicopter_dynamics.py:400-489) at stage state s, with committed
  * ground height h_c (F6).  Writes the 18 derivatives; if obs != NULL also the observation
  * (:471-488). */
@@ -555,7 +563,9 @@ void or_dynamics_c(const or_model* m, const double s[18], const controls* u, con
             pos[i] = xyz[i] + (double)br;
             vel[i] = ned[i] + (B[0][i] * wxr[0] + B[1][i] * wxr[1] + B[2][i] * wxr[2]);
         }
-        if ((-pos[2]) - h_touch < 0.0) {
+        double clearance = (-pos[2]) - h_touch;
+        if (fabs(clearance) < g_lg_margin) g_lg_margin = fabs(clearance);
+        if (clearance < 0.0) {
             double fz = -(a->lg_C * vel[2] + a->lg_K * (pos[2] + h_c)) + EPS_DYN;
             for (int i = 0; i < 3; i++) F_lg[i] += B[i][2] * fz;
             double mm[3];

@@ -73,6 +73,7 @@ class Oracle:
         lib.or_trim.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.hg_trim_cond), PD,
                                 ctypes.POINTER(_abi.hg_trim_result)]
         lib.or_reset.argtypes = [ctypes.c_void_p, ctypes.POINTER(or_env), ctypes.POINTER(_abi.hg_trim_result)]
+        lib.or_diag_lg_margin.restype = D
         lib.or_rollout.restype = ctypes.c_int64
         lib.or_rollout.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.hg_trim_result), ctypes.c_int64,
                                    ctypes.c_int64, ctypes.c_uint64, PD]
@@ -147,7 +148,9 @@ class Oracle:
         a = np.ascontiguousarray(action, dtype=np.float64)
         n = np.ascontiguousarray(eta, dtype=np.float64)
         o = or_out()
+        self.lib.or_diag_reset()
         self.lib.or_step(self.m, ctypes.byref(e), _dp(a), _dp(n), ctypes.byref(o))
+        self.last_lg_margin = self.lib.or_diag_lg_margin()
         return o
 
     def rollout(self, tr, n_envs, n_steps, seed=0):

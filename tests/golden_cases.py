@@ -1,0 +1,95 @@
+"""Turn the golden trajectories (tests/golden/traj_dt*.npz, recorded from the reference by
+tools/gen_goldens.py) into batched single-step cases: one env per recorded step, its pre-step
+state taken from the reference itself.  Data only — no oracle, no reference code."""
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TASK_KEY = {"hover": "success_hover", "forward_flight": "success_ff"}
+REWARD_KEY = {"hover": "reward_hover", "forward_flight": "reward_ff"}
+
+
+def success_threshold(dt, max_time=40.0):
+    """Steps of success needed for `successed` (helicopter.py:205,236-237 float accumulation)."""
+    s, k = 0.0, 0
+    while not s >= max_time / 4:
+        s += dt
+        k += 1
+    return k
+
+
+def time_up_threshold(dt, max_time=40.0):
+    t, k = 0.0, 0
+    while not t > max_time:
+        t += dt
+        k += 1
+    return k
+
+
+def load(tag):
+    return np.load(os.path.join(GOLDEN, f"traj_dt{tag}.npz"), allow_pickle=False)
+
+
+def single_step_batch(d, task="hover"):
+    dt = float(d["dt"])
+    n_succ = success_threshold(dt)
+    n_up = time_up_threshold(dt)
+    rows = {k: [] for k in ("state", "counters", "actions", "eta", "obs", "heli", "wind", "reward",
+                            "failed", "successed", "time_up", "terminated", "truncated", "success_step",
+                            "dots", "scenario", "t")}
+    for n in d["scenarios"]:
+        g = lambda k: d[f"{n}/{k}"]  # noqa: E731
+        T = len(g("reward_hover"))
+        succ_flags = g(TASK_KEY[task])
+        for t in range(T):
+            if t == 0:
+                heli, wind, prev_obs = g("init_state"), g("init_wind_state"), g("init_obs")
+            else:
+                heli, wind, prev_obs = g("state")[t - 1], g("wind_state")[t - 1], g("obs")[t - 1]
+            carry = [prev_obs[4], prev_obs[5], prev_obs[6], prev_obs[16]]
+            succ_before = int(np.sum(succ_flags[:t]))
+            rows["state"].append(np.concatenate([heli, wind, carry]))
+            rows["counters"].append([t, succ_before, 0])
+            rows["actions"].append(g("action")[t])
+            rows["eta"].append(g("eta")[t])
+            rows["obs"].append(g("obs")[t])
+            rows["heli"].append(g("state")[t])
+            rows["wind"].append(g("wind_state")[t])
+            rows["dots"].append(g("state_dots")[t])
+            rows["reward"].append(g(REWARD_KEY[task])[t])
+            failed = bool(g("failed")[t])
+            successed = succ_before >= n_succ
+            time_up = (t + 1) >= n_up
+            rows["failed"].append(failed)
+            rows["successed"].append(successed)
+            rows["time_up"].append(time_up)
+            rows["terminated"].append(failed or successed)
+            rows["truncated"].append(time_up)
+            rows["success_step"].append(bool(succ_flags[t]))
+            rows["scenario"].append(str(n))
+            rows["t"].append(t)
+    out = {k: np.array(v) for k, v in rows.items()}
+    out["dt"] = dt
+    return out
+
+
+def step_errors(got, ref, angle_cols=()):
+    """|got - ref| with angle columns compared modulo 2*pi."""
+    d = np.abs(np.asarray(got, dtype=np.float64) - np.asarray(ref, dtype=np.float64))
+    for c in angle_cols:
+        d[..., c] = np.minimum(d[..., c], np.abs(d[..., c] - 2 * np.pi))
+    return d
+
+
+HELI_ANGLE_COLS = (2, 3, 4, 5, 12, 13, 14)   # psi_mr psi_tr betas euler (wrapped, utils.py:3-4)
+OBS_ANGLE_COLS = (7, 8, 9)
+
+
+def edge_distance_ft(x, y, rows=1024, span=6561.6798):
+    """Distance (ft) of a position from the nearest terrain cell edge of the reference's height
+    map (helicopter_dynamics.py:168-186), where its ground height is discontinuous."""
+    px = span / rows
+    fx = (x / px) % 1.0
+    fy = (y / px) % 1.0
+    return px * min(fx, 1 - fx, fy, 1 - fy)

@@ -1,0 +1,108 @@
+"""CPU-side checks of the product library: it loads, exports every symbol include/heligym_amd.h
+declares, its host trim (the reset template) matches the reference's trim, and argument errors
+are reported through error codes.  No device calls."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, load_golden, trim_dict
+
+from heligym_amd import _abi, config
+
+HEADER = os.path.join(ROOT, "include", "heligym_amd.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return _abi.load_library()
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(hg_[a-z_0-9]+)\s*\(", txt)))
+
+
+def test_exports_every_declared_symbol(lib):
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert sorted(_abi.EXPORTED_SYMBOLS) == syms
+
+
+def test_struct_layout_matches_header(lib):
+    # hg_default_config writes the AW109 defaults through the C struct: compare with our yaml
+    c = _abi.hg_config()
+    lib.hg_default_config(ctypes.byref(c))
+    y, _ = config.make_config()
+    for name, _ in _abi.hg_airframe._fields_:
+        assert getattr(c.af, name) == getattr(y.af, name), name
+    assert c.dt == y.dt and c.max_time == y.max_time and c.task == y.task
+    assert c.trim.gr_alt == 100.0 and c.target.sea_alt == 4000.0
+    assert ctypes.sizeof(_abi.hg_trim_result) == 8 * (18 + 4 + 17 + 18 + 1) + 8
+
+
+@pytest.mark.parametrize("i", range(16))
+def test_host_trim_matches_reference(lib, terrain_u16, i):
+    t = load_golden("trim.npz")
+    cfg, _ = config.make_config(dt=float(t["dt"][i]), trim_cond=trim_dict(t["cond"][i]))
+    hm = config.terrain_ft(terrain_u16, cfg.af.env_MAX_GR_ALT)
+    w = (ctypes.c_double * 3)(*t["wind_ned"][i])
+    r = _abi.hg_trim_result()
+    _abi.check(lib.hg_trim(ctypes.byref(cfg), hm.ctypes.data, 1024, 1024, w, ctypes.byref(r)), lib)
+    for name in ("state", "action", "obs"):
+        got, ref = np.array(getattr(r, name)), t[name][i]
+        assert np.all(np.abs(got - ref) <= 1e-4 * (np.abs(ref) + 1)), (name, got - ref)
+    assert r.residual <= 1e-4 and not r.failed
+
+
+def test_host_trim_second_episode_wind(lib, terrain_u16):
+    t = load_golden("trim.npz")
+    cfg, _ = config.make_config(dt=0.02)
+    hm = config.terrain_ft(terrain_u16, cfg.af.env_MAX_GR_ALT)
+    w = (ctypes.c_double * 3)(*t["reset2_wind_ned"])
+    r = _abi.hg_trim_result()
+    _abi.check(lib.hg_trim(ctypes.byref(cfg), hm.ctypes.data, 1024, 1024, w, ctypes.byref(r)), lib)
+    assert np.all(np.abs(np.array(r.state) - t["reset2_state"]) <= 1e-4 * (np.abs(t["reset2_state"]) + 1))
+
+
+def test_errors_are_codes_not_crashes(lib, terrain_u16):
+    cfg, _ = config.make_config()
+    hm = config.terrain_ft(terrain_u16, cfg.af.env_MAX_GR_ALT)
+    h = ctypes.c_void_p()
+    bad = _abi.hg_config.from_buffer_copy(cfg)
+    bad.dt = -1.0
+    assert lib.hg_create(ctypes.byref(bad), hm.ctypes.data, 1024, 1024, 16, ctypes.byref(h)) == -1
+    assert b"dt" in lib.hg_last_error()
+    assert lib.hg_create(ctypes.byref(cfg), hm.ctypes.data, 1024, 1024, 0, ctypes.byref(h)) == -1
+    assert lib.hg_create(ctypes.byref(cfg), hm.ctypes.data, 1024, 512, 16, ctypes.byref(h)) == -1
+    bad = _abi.hg_config.from_buffer_copy(cfg)
+    bad.task = 9
+    assert lib.hg_create(ctypes.byref(bad), hm.ctypes.data, 1024, 1024, 16, ctypes.byref(h)) == -1
+    assert lib.hg_step(None, None, None, None, None, None, None, None, None, None, None, None) == -1
+    assert lib.hg_reset(None, None, None, None) == -1
+    assert lib.hg_num_envs(None) == -1
+    # impossible trim condition: the reference asserts after 5 s (helicopter_dynamics.py:543-544)
+    wild = _abi.hg_config.from_buffer_copy(cfg)
+    wild.trim.ned_vel[0] = 5000.0
+    r = _abi.hg_trim_result()
+    rc = lib.hg_trim(ctypes.byref(wild), hm.ctypes.data, 1024, 1024, None, ctypes.byref(r))
+    assert rc in (0, -3)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(_abi.HeliGymError):
+        _abi.load_library(str(tmp_path / "nope.so"))
+
+
+def test_vector_env_refuses_without_device():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    from heligym_amd import HeliVecEnv
+    with pytest.raises(_abi.HeliGymError):
+        HeliVecEnv(8)

@@ -1,0 +1,262 @@
+"""GPU parity: the gfx950 step kernel (through the C-ABI) against the reference's own recorded
+steps (tests/golden) and against the oracle (oracle/heli_oracle.c).  Run with -m gpu."""
+import numpy as np
+import pytest
+
+import golden_cases as gc
+
+pytestmark = pytest.mark.gpu
+
+# SURVEY 8(a) parity contract, fp32 kernel vs the reference's mixed fp32/fp64 step:
+STEP_ABS, STEP_REL = 2e-4, 2e-5        # (i) one step from identical inputs
+TRAJ_ABS, TRAJ_REL = 1e-3, 1e-4        # (ii) 100-step trajectories with injected eta, pre-contact
+TRIM_REL = 1e-4                        # (iii) |d| <= 1e-4 (|x| + 1)
+REWARD_ABS, REWARD_REL = 2e-4, 2e-5
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no HIP device")
+    return t
+
+
+def make_env(torch, n, task, dt, autoreset=False, **kw):
+    from heligym_amd import HeliVecEnv
+    return HeliVecEnv(n, task=task, dt=dt, autoreset=autoreset, device="cuda:0",
+                      target={"vel": 100.0, "heading": 0.0} if task == "forward_flight" else None, **kw)
+
+
+def run_single_steps(torch, batch, task):
+    env = make_env(torch, len(batch["state"]), task, batch["dt"])
+    env.set_state(batch["state"].astype(np.float32), batch["counters"].astype(np.int32))
+    act = torch.as_tensor(batch["actions"].astype(np.float32), device=env.device)
+    eta = torch.as_tensor(batch["eta"].astype(np.float32), device=env.device)
+    obs, rew, term, trunc, info = env.step(act, eta=eta)
+    st, ctr = env.get_state()
+    torch.cuda.synchronize()
+    out = {"obs": obs.cpu().numpy().astype(np.float64), "reward": rew.cpu().numpy().astype(np.float64),
+           "terminated": term.cpu().numpy(), "truncated": trunc.cpu().numpy(),
+           "state": st.cpu().numpy().astype(np.float64), "counters": ctr.cpu().numpy()}
+    for k in ("failed", "successed", "time_up", "success_step"):
+        out[k] = info[k].cpu().numpy()
+    env.close()
+    return out
+
+
+@pytest.mark.parametrize("tag", ["0.02", "0.01"])
+@pytest.mark.parametrize("task", ["hover", "forward_flight"])
+def test_single_step_vs_reference(torch, tag, task):
+    b = gc.single_step_batch(gc.load(tag), task)
+    out = run_single_steps(torch, b, task)
+    e_obs = gc.step_errors(out["obs"], b["obs"], gc.OBS_ANGLE_COLS)
+    e_heli = gc.step_errors(out["state"][:, :18], b["heli"], gc.HELI_ANGLE_COLS)
+    e_wind = gc.step_errors(out["state"][:, 18:23], b["wind"])
+    tol_obs = STEP_ABS + STEP_REL * np.abs(b["obs"])
+    tol_heli = STEP_ABS + STEP_REL * np.abs(b["heli"])
+    tol_wind = STEP_ABS + STEP_REL * np.abs(b["wind"])
+    print(f"\n[{task} dt={tag}] {len(b['obs'])} steps: max|d obs| {e_obs.max():.3e}  "
+          f"max|d state| {e_heli.max():.3e}  max|d wind| {e_wind.max():.3e}  "
+          f"max|d reward| {np.abs(out['reward'] - b['reward']).max():.3e}")
+    bad = np.argwhere(e_obs > tol_obs)
+    assert len(bad) == 0, [(b["scenario"][i], b["t"][i], c, e_obs[i, c]) for i, c in bad[:10]]
+    bad = np.argwhere(e_heli > tol_heli)
+    assert len(bad) == 0, [(b["scenario"][i], b["t"][i], c, e_heli[i, c]) for i, c in bad[:10]]
+    assert np.all(e_wind <= tol_wind)
+    # carry = this step's observation (next step's wind input, helicopter.py:195-196)
+    np.testing.assert_allclose(out["state"][:, 23:26], out["obs"][:, 4:7], rtol=0, atol=0)
+    np.testing.assert_allclose(out["state"][:, 26], out["obs"][:, 16], rtol=0, atol=0)
+    e_rew = np.abs(out["reward"] - b["reward"])
+    assert np.all(e_rew <= REWARD_ABS + REWARD_REL * np.abs(b["reward"])), e_rew.max()
+    for k in ("failed", "successed", "time_up", "terminated", "truncated", "success_step"):
+        mism = np.nonzero(out[k].astype(bool) != b[k].astype(bool))[0]
+        assert len(mism) == 0, (k, [(b["scenario"][i], b["t"][i]) for i in mism[:10]])
+    np.testing.assert_array_equal(out["counters"][:, 0], b["counters"][:, 0] + 1)
+    np.testing.assert_array_equal(out["counters"][:, 1], b["counters"][:, 1] + b["success_step"])
+
+
+@pytest.mark.parametrize("tag", ["0.02", "0.01"])
+def test_single_step_vs_oracle(torch, tag, terrain_u16):
+    """Same inputs (rounded to fp32 for both) through the oracle: checks the kernel against the
+    CPU restatement independently of the reference's own rounding."""
+    from heligym_amd import config
+    from oracle.oracle import Oracle
+    b = gc.single_step_batch(gc.load(tag), "hover")
+    out = run_single_steps(torch, b, "hover")
+    cfg, _ = config.make_config(task="hover", dt=b["dt"])
+    orc = Oracle(cfg, terrain_u16)
+    st32 = b["state"].astype(np.float32).astype(np.float64)
+    worst = 0.0
+    for i in range(len(st32)):
+        s = st32[i]
+        prev_obs = np.zeros(17)
+        prev_obs[4:7], prev_obs[16] = s[23:26], s[26]
+        e = orc.env_from(s[:18], s[18:23], prev_obs, np.zeros(18), 0.0, 0.0)
+        o = orc.step(e, b["actions"][i].astype(np.float32), b["eta"][i].astype(np.float32))
+        d = gc.step_errors(out["obs"][i], np.array(o.obs), gc.OBS_ANGLE_COLS)
+        assert np.all(d <= STEP_ABS + STEP_REL * np.abs(np.array(o.obs))), (b["scenario"][i], b["t"][i], d)
+        d2 = gc.step_errors(out["state"][i, :18], np.array(e.heli), gc.HELI_ANGLE_COLS)
+        assert np.all(d2 <= STEP_ABS + STEP_REL * np.abs(np.array(e.heli))), (b["scenario"][i], b["t"][i], d2)
+        assert abs(out["reward"][i] - o.reward_hover) <= REWARD_ABS + REWARD_REL * abs(o.reward_hover)
+        assert bool(out["failed"][i]) == bool(o.failed)
+        worst = max(worst, d.max(), d2.max())
+    print(f"\n[oracle dt={tag}] max abs diff {worst:.3e}")
+
+
+@pytest.mark.parametrize("tag", ["0.02", "0.01"])
+def test_trajectories_100_steps(torch, tag):
+    """Each scenario replayed for 100 steps from the reference's reset state with its actions and
+    turbulence noise: one env per scenario, the kernel carries its own fp32 state."""
+    d = gc.load(tag)
+    scen = [str(s) for s in d["scenarios"]]
+    T = 100
+    env = make_env(torch, len(scen), "hover", float(d["dt"]))
+    st = np.stack([np.concatenate([d[f"{n}/init_state"], d[f"{n}/init_wind_state"],
+                                   d[f"{n}/init_obs"][[4, 5, 6, 16]]]) for n in scen])
+    env.set_state(st.astype(np.float32), np.zeros((len(scen), 3), np.int32))
+    worst = {}
+    alive = np.ones(len(scen), bool)
+    for t in range(T):
+        acts, etas = np.zeros((len(scen), 4), np.float32), np.zeros((len(scen), 3), np.float32)
+        for j, n in enumerate(scen):
+            if t < len(d[f"{n}/action"]):
+                acts[j], etas[j] = d[f"{n}/action"][t], d[f"{n}/eta"][t]
+            else:
+                alive[j] = False
+        obs, *_ = env.step(torch.as_tensor(acts, device=env.device), eta=torch.as_tensor(etas, device=env.device))
+        o = obs.cpu().numpy().astype(np.float64)
+        for j, n in enumerate(scen):
+            if not alive[j]:
+                continue
+            ref = d[f"{n}/obs"][t]
+            if ref[16] < 10.0:   # pre-contact only (contract ii); landing-gear contact is stiff
+                alive[j] = False
+                continue
+            err = gc.step_errors(o[j], ref, gc.OBS_ANGLE_COLS)
+            # The reference's ground height jumps across terrain cell edges (three-point scheme,
+            # helicopter_dynamics.py:185-194); where the committed position lies within the
+            # trajectory's position error of an edge, GROUND_ALTITUDE may sit on the other side.
+            prev = d[f"{n}/state"][t - 1] if t else d[f"{n}/init_state"]
+            if gc.edge_distance_ft(prev[15], prev[16]) < 1e-2:
+                err[16] = 0.0
+            assert np.all(err <= TRAJ_ABS + TRAJ_REL * np.abs(ref)), (n, t, err)
+            worst[n] = max(worst.get(n, 0.0), float((err / (TRAJ_ABS + TRAJ_REL * np.abs(ref))).max()))
+    env.close()
+    print("\n[trajectory] worst error / tolerance per scenario:", {k: round(v, 3) for k, v in worst.items()})
+
+
+def test_reset_template_vs_reference_trim(torch):
+    from conftest import load_golden, trim_dict
+    t = load_golden("trim.npz")
+    for i in range(len(t["dt"])):
+        env = make_env(torch, 4, "hover", float(t["dt"][i]), trim_cond=trim_dict(t["cond"][i]))
+        tr = env.template()
+        for name in ("state", "action", "obs"):
+            assert np.all(np.abs(tr[name] - t[name][i]) <= TRIM_REL * (np.abs(t[name][i]) + 1)), (i, name)
+        obs, info = env.reset()
+        np.testing.assert_allclose(obs.cpu().numpy(), np.tile(tr["obs"].astype(np.float32), (4, 1)))
+        env.close()
+
+
+def test_autoreset_and_compaction(torch):
+    """Same-step auto-reset: a twin env without auto-reset, fed the same actions, gives the terminal
+    observation each env's first episode must report in info["final_obs"]."""
+    N = 4096
+    env = make_env(torch, N, "hover", 0.02, autoreset=True, seed=7)
+    twin = make_env(torch, N, "hover", 0.02, autoreset=False, seed=7)
+    env.reset()
+    twin.reset()
+    tmpl_obs = env.template()["obs"].astype(np.float32)
+    act = torch.empty((N, 4), dtype=torch.float32, device=env.device)
+    total = 0
+    first_done = np.zeros(N, bool)
+    for k in range(700):
+        env.random_actions(act, seed=3, step=k)
+        obs, rew, term, trunc, info = env.step(act)
+        tobs, *_ = twin.step(act)
+        idx = info["reset_index"].cpu().numpy()
+        done = (term | trunc).cpu().numpy()
+        np.testing.assert_array_equal(np.sort(idx), np.nonzero(done)[0])
+        if len(idx):
+            o = obs.cpu().numpy()
+            np.testing.assert_array_equal(o[idx], np.tile(tmpl_obs, (len(idx), 1)))
+            fo = info["final_obs"].cpu().numpy()
+            to = tobs.cpu().numpy()
+            new = ~first_done[idx]
+            np.testing.assert_array_equal(fo[new], to[idx[new]])
+            first_done[idx] = True
+            assert np.all(info["failed"].cpu().numpy()[idx] | info["successed"].cpu().numpy()[idx]
+                          | info["time_up"].cpu().numpy()[idx])
+        total += len(idx)
+    _, ctr = env.get_state()
+    c = ctr.cpu().numpy()
+    assert total > N // 2                      # U(-1,1) episodes end after ~500 steps
+    assert c[:, 2].sum() == total + N          # episode counter: reset() + every auto-reset
+    env.close()
+    twin.close()
+
+
+def test_determinism_and_sharding(torch):
+    """Same seed -> bitwise identical; env j of a shard with env_offset=o equals env o+j of the
+    full batch (the Philox stream is keyed by global env id)."""
+    N, K = 2048, 50
+
+    def run(n, offset):
+        env = make_env(torch, n, "hover", 0.01, autoreset=True, seed=11, env_offset=offset)
+        env.reset()
+        act = torch.empty((n, 4), dtype=torch.float32, device=env.device)
+        for k in range(K):
+            env.random_actions(act, seed=5, step=k)
+            obs, *_ = env.step(act)
+        s, c = env.get_state()
+        res = (obs.cpu().numpy().copy(), s.cpu().numpy().copy())
+        env.close()
+        return res
+
+    a = run(N, 0)
+    b = run(N, 0)
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[1], b[1])
+    c = run(N // 2, N // 2)
+    np.testing.assert_array_equal(a[0][N // 2:], c[0])
+    np.testing.assert_array_equal(a[1][N // 2:], c[1])
+
+
+def test_full_size_invariants(torch):
+    """BASELINE config 3 size (65 536 envs, dt 0.01, turbulence on): size-independent properties."""
+    N = 65536
+    env = make_env(torch, N, "hover", 0.01, autoreset=True, seed=1)
+    obs, _ = env.reset()
+    act = torch.empty((N, 4), dtype=torch.float32, device=env.device)
+    resets = 0
+    for k in range(200):
+        env.random_actions(act, seed=2, step=k)
+        obs, rew, term, trunc, info = env.step(act)
+        resets += len(info["reset_index"])
+    torch.cuda.synchronize()
+    o = obs.cpu().numpy()
+    assert np.all(np.isfinite(o))
+    assert np.all(np.isfinite(rew.cpu().numpy()))
+    s, c = env.get_state()
+    s = s.cpu().numpy()
+    c = c.cpu().numpy()
+    # wrapped angles stay in [-pi, pi) (utils.py:3-4)
+    for col in gc.HELI_ANGLE_COLS:
+        assert s[:, col].min() >= -np.pi - 1e-6 and s[:, col].max() < np.pi + 1e-6
+    # carry is the last observation
+    np.testing.assert_array_equal(s[:, 23:26], o[:, 4:7])
+    assert np.all(c[:, 0] <= 200) and np.all(c[:, 1] <= c[:, 0])
+    env.close()
+
+
+def test_single_env_dropin(torch):
+    from heligym_amd import HeliHover
+    env = HeliHover(dt=0.02)
+    obs, info = env.reset()
+    assert obs.shape == (17,) and obs.dtype == np.float32 and set(info) == {"failed", "successed", "time_up"}
+    t = gc.load("0.02")
+    np.testing.assert_allclose(obs, t["hover_zero/init_obs"], rtol=1e-4, atol=1e-3)
+    obs, r, term, trunc, info = env.step(np.zeros(4, np.float32))
+    assert isinstance(r, float) and isinstance(term, bool) and isinstance(trunc, bool)
+    env.close()
