@@ -30,6 +30,10 @@ namespace {
 
 thread_local std::string g_last_error;
 
+void dfree(void* p) {
+    if (p) (void)hipFree(p);
+}
+
 int32_t fail(int32_t code, const std::string& msg) {
     g_last_error = msg;
     return code;
@@ -91,10 +95,27 @@ struct StepArgs {
     int64_t env_offset;
 };
 
+#ifndef HG_PARAMS_PTR
+#define HG_PARAMS_PTR 1
+#endif
+#ifndef HG_RK_LOOP
+#define HG_RK_LOOP 0
+#endif
+#if HG_PARAMS_PTR
+using ParamArg = const Params<float>* __restrict__;
+#else
+using ParamArg = const Params<float>;
+#endif
+
 template <int TASK>
-__global__ __launch_bounds__(kBlock) void step_kernel(const Params<float> P, const Template<float> T,
+__global__ __launch_bounds__(kBlock) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
     __shared__ float s_obs[kBlock * HG_N_OBS];
+#if HG_PARAMS_PTR
+    const Params<float>& P = *Pa;   // model constants: scalar loads from a device copy
+#else
+    const Params<float>& P = Pa;
+#endif
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * kBlock;
     const int64_t i = blk0 + tid;
@@ -139,6 +160,20 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Params<float> P, con
     // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
     const hg::Controls<float> u = hg::controls(P, act.x, act.y, act.z, act.w);
     float k[18], acc[18], st[18], obs[17];
+#if HG_RK_LOOP
+#pragma unroll
+    for (int c = 0; c < 18; ++c) { acc[c] = 0.f; st[c] = hs[c]; }
+#pragma unroll 1
+    for (int stage = 0; stage < 4; ++stage) {
+        hg::dynamics<true>(P, st, u, W, h_c, k, obs);
+        const float w = (stage == 0 || stage == 3) ? 1.f : 2.f;
+        const float cn = stage == 2 ? P.dt : P.half_dt;
+#pragma unroll
+        for (int c = 0; c < 18; ++c) { acc[c] += w * k[c]; st[c] = hs[c] + k[c] * cn; }
+    }
+#pragma unroll
+    for (int c = 0; c < 18; ++c) hs[c] = hs[c] + acc[c] * P.dt6;
+#else
     hg::dynamics<false>(P, hs, u, W, h_c, k, obs);
 #pragma unroll
     for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
@@ -151,6 +186,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Params<float> P, con
     hg::dynamics<true>(P, st, u, W, h_c, k, obs);
 #pragma unroll
     for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
+#endif
     // step_after (helicopter_dynamics.py:73-77)
     hs[2] = hg::pi_bound(hs[2]);
     hs[3] = hg::pi_bound(hs[3]);
@@ -204,6 +240,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(const Params<float> P, con
         }
     }
     if (do_reset) {
+        const Template<float>& T = *Tp;   // reset template in HBM (read only by resetting lanes)
 #pragma unroll
         for (int c = 0; c < 18; ++c) hs[c] = T.heli[c];
 #pragma unroll
@@ -600,8 +637,18 @@ struct hg_env {
     Params<float> Pf;
     Params<double> Pd;
     Template<float> tmpl;
+    Template<float>* tmpl_dev = nullptr;
+    Params<float>* params_dev = nullptr;
     hg_trim_result trim;
 };
+
+// Upload the fp32 model constants the step kernel reads (after create and every setter).
+static int32_t upload_params(hg_env* e) {
+    if (!e->params_dev) return HG_OK;
+    hipError_t err = hipMemcpy(e->params_dev, &e->Pf, sizeof(e->Pf), hipMemcpyHostToDevice);
+    if (err != hipSuccess) return fail(HG_E_HIP, std::string("params upload: ") + hipGetErrorString(err));
+    return HG_OK;
+}
 
 static int32_t build_template(hg_env* e) {
     const double W[3] = {e->Pd.wm[0], e->Pd.wm[1], e->Pd.wm[2]};   // helicopter.py:55 (mean wind)
@@ -616,10 +663,20 @@ static int32_t build_template(hg_env* e) {
     e->tmpl.carry[1] = (float)r.obs[5];
     e->tmpl.carry[2] = (float)r.obs[6];
     e->tmpl.carry[3] = (float)r.obs[16];
+    if (e->tmpl_dev) {   // device copy read by the step kernel's auto-reset (stream-ordered after prior work)
+        hipError_t err = hipMemcpy(e->tmpl_dev, &e->tmpl, sizeof(e->tmpl), hipMemcpyHostToDevice);
+        if (err != hipSuccess) return fail(HG_E_HIP, std::string("template upload: ") + hipGetErrorString(err));
+    }
     return HG_OK;
 }
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+#if HG_PARAMS_PTR
+#define PARAM_ARG(e) ((const Params<float>*)(e)->params_dev)
+#else
+#define PARAM_ARG(e) ((e)->Pf)
+#endif
 
 extern "C" {
 
@@ -699,7 +756,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     rc = build_template(e);
     if (rc != HG_OK) { delete e; return rc; }
     auto cleanup = [&](hipError_t err, const char* what) {
-        hipFree(e->hmap); hipFree(e->state); hipFree(e->counters);
+        dfree(e->hmap); dfree(e->state); dfree(e->counters); dfree(e->tmpl_dev); dfree(e->params_dev);
         delete e;
         return fail(HG_E_HIP, std::string(what) + ": " + hipGetErrorString(err));
     };
@@ -709,6 +766,12 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if ((err = hipMalloc(&e->counters, sizeof(int32_t) * kCtrCols * num_envs)) != hipSuccess) return cleanup(err, "hipMalloc counters");
     if ((err = hipMemcpy(e->hmap, e->hmap_host.data(), sizeof(float2) * rows * cols, hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy terrain");
+    if ((err = hipMalloc(&e->params_dev, sizeof(Params<float>))) != hipSuccess) return cleanup(err, "hipMalloc params");
+    if ((err = hipMemcpy(e->params_dev, &e->Pf, sizeof(e->Pf), hipMemcpyHostToDevice)) != hipSuccess)
+        return cleanup(err, "hipMemcpy params");
+    if ((err = hipMalloc(&e->tmpl_dev, sizeof(Template<float>))) != hipSuccess) return cleanup(err, "hipMalloc template");
+    if ((err = hipMemcpy(e->tmpl_dev, &e->tmpl, sizeof(e->tmpl), hipMemcpyHostToDevice)) != hipSuccess)
+        return cleanup(err, "hipMemcpy template");
     hipLaunchKernelGGL(init_kernel, dim3(grid_for(num_envs)), dim3(kBlock), 0, 0, e->tmpl, e->state, e->counters, num_envs);
     if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "init_kernel");
     if ((err = hipDeviceSynchronize()) != hipSuccess) return cleanup(err, "init sync");
@@ -718,9 +781,11 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
 
 void hg_destroy(hg_env* e) {
     if (!e) return;
-    hipFree(e->hmap);
-    hipFree(e->state);
-    hipFree(e->counters);
+    dfree(e->hmap);
+    dfree(e->state);
+    dfree(e->counters);
+    dfree(e->tmpl_dev);
+    dfree(e->params_dev);
     delete e;
 }
 
@@ -731,7 +796,7 @@ int32_t hg_set_max_time(hg_env* e, double max_time) {
     e->cfg.max_time = max_time;
     e->Pd = derive<double>(e->cfg, e->rows, e->cols);
     e->Pf = derive<float>(e->cfg, e->rows, e->cols);
-    return HG_OK;
+    return upload_params(e);
 }
 
 int32_t hg_set_target(hg_env* e, const hg_target* t) {
@@ -739,7 +804,7 @@ int32_t hg_set_target(hg_env* e, const hg_target* t) {
     e->cfg.target = *t;
     e->Pd = derive<double>(e->cfg, e->rows, e->cols);
     e->Pf = derive<float>(e->cfg, e->rows, e->cols);
-    return HG_OK;
+    return upload_params(e);
 }
 
 int32_t hg_set_trim_cond(hg_env* e, const hg_trim_cond* tc) {
@@ -797,13 +862,13 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     const dim3 grid(grid_for(e->n)), block(kBlock);
     switch (e->cfg.task) {
         case HG_TASK_HOVER:
-            hipLaunchKernelGGL(step_kernel<HG_TASK_HOVER>, grid, block, 0, s, e->Pf, e->tmpl, a);
+            hipLaunchKernelGGL(step_kernel<HG_TASK_HOVER>, grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);
             break;
         case HG_TASK_FORWARD_FLIGHT:
-            hipLaunchKernelGGL(step_kernel<HG_TASK_FORWARD_FLIGHT>, grid, block, 0, s, e->Pf, e->tmpl, a);
+            hipLaunchKernelGGL(step_kernel<HG_TASK_FORWARD_FLIGHT>, grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);
             break;
         default:
-            hipLaunchKernelGGL(step_kernel<HG_TASK_HELI>, grid, block, 0, s, e->Pf, e->tmpl, a);
+            hipLaunchKernelGGL(step_kernel<HG_TASK_HELI>, grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);
             break;
     }
     HIP_TRY(hipGetLastError());

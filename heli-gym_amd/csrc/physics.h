@@ -25,7 +25,30 @@ HD float m_floor(float x) { return floorf(x); }
 HD double m_floor(double x) { return floor(x); }
 HD float m_fmod(float x, float y) { return fmodf(x, y); }
 HD double m_fmod(double x, double y) { return fmod(x, y); }
-HD void m_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+// fp32 sin/cos for the attitude angles (|x| <= ~4 rad: wrapped euler angles plus one RK stage
+// increment): Cody-Waite reduction by pi/2 (3-part constant) and minimax polynomials on
+// [-pi/4, pi/4]; ~1 ulp, ~25 VALU ops for both, no Payne-Hanek slow path (libm sincosf spills a
+// 36-byte scratch table for it).  Larger |x| keeps working with degrading absolute accuracy.
+HD void m_sincos(float x, float* s, float* c) {
+    const float k = rintf(x * 0.636619772367581343f);
+    float r = fmaf(k, -1.57079637050628662109375f, x);
+    r = fmaf(k, 4.37113900018624283e-8f, r);
+    r = fmaf(k, 1.71512451e-15f, r);
+    const float r2 = r * r;
+    // sin(r) ~ r + r^3 (s1 + r^2 (s2 + r^2 s3)), cos(r) ~ 1 + r^2 (c1 + r^2 (c2 + r^2 (c3 + r^2 c4)))
+    float sp = fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+    sp = fmaf(r2, sp, -1.6666654611e-1f);
+    const float sr = fmaf(r * r2, sp, r);
+    float cp = fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    cp = fmaf(r2, cp, 4.166664568298827e-2f);
+    cp = fmaf(r2, cp, -0.5f);
+    const float cr = fmaf(r2, cp, 1.0f);
+    const int q = (int)k;
+    const bool swap = q & 1;
+    const float ss = swap ? cr : sr, cc = swap ? sr : cr;
+    *s = (q & 2) ? -ss : ss;
+    *c = ((q + 1) & 2) ? -cc : cc;
+}
 HD void m_sincos(double x, double* s, double* c) { *s = sin(x); *c = cos(x); }
 // x^e for x > 0 (ISA density ratio, Dryden scale lengths)
 HD float m_pow(float x, float e) { return exp2f(e * log2f(x)); }
@@ -111,8 +134,9 @@ HD Controls<R> controls(const Params<R>& P, R a0, R a1, R a2, R a3) {
 template <typename R>
 HD R pi_bound(R x) {
     const R twopi = (R)(2 * kPi);
-    R r = m_fmod(x + (R)kPi, twopi);
-    r = r < (R)0 ? r + twopi : r;
+    R r = x + (R)kPi;
+    r = r - twopi * m_floor(r * (R)(1.0 / (2 * kPi)));   // floor-mod, one step
+    r = r < (R)0 ? r + twopi : (r >= twopi ? r - twopi : r);
     return r - (R)kPi;
 }
 

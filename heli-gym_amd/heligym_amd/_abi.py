@@ -8,7 +8,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libheligym_amd.so")
+LIB_PATH = os.environ.get("HELIGYM_AMD_LIB") or os.path.join(_HERE, "libheligym_amd.so")
 
 HG_N_OBS = 17
 HG_N_ACT = 4

