@@ -46,6 +46,23 @@ def parse():
     return ap.parse_args()
 
 
+def pmc_traffic(envs, dt, task):
+    """HBM bytes per step-kernel launch from the newest committed PMC summary for this workload
+    (profiles/<tag>_pmc_summary.json, written by scripts/summarize_prof.py from rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes).  None if this workload was not profiled."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("envs") == envs and abs(d.get("dt", -1) - dt) < 1e-12 and task == "hover" \
+                and "hbm_bytes_per_launch" in d:
+            best = (d["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best
+
+
 def cpu_baseline(dt, task, seconds):
     """Oracle (C restatement, 1 thread) on a bounded sample of the same workload."""
     from heligym_amd import config
@@ -172,9 +189,11 @@ def main():
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     elapsed = float(el_t[0])
 
-    # per-launch kernel duration on the env's stream (HIP events around single launches)
+    # per-launch kernel duration on the env's stream: HIP events around single launches, queued
+    # behind a spin kernel so the GPU runs event/kernel/event back to back (no host gaps inside)
     n_ev = 50
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    torch.cuda._sleep(int(2e7))
     for j, (a, b) in enumerate(evs):
         a.record()
         env.step_async(bank[j % B], with_reset_info=False)
@@ -209,10 +228,15 @@ def main():
                    "envs_per_gpu": N, "dt": args.dt, "task": args.task, "parallelism": f"env-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "step_kernel<HOVER>", "kernel_avg_us": kern_s * 1e6,
-                     "bytes_per_env_step": BYTES_PER_ENV_STEP},
+                     "kernel": f"step_kernel<{args.task.upper()}>", "kernel_avg_us": kern_s * 1e6,
+                     "bytes_per_env_step": BYTES_PER_ENV_STEP,
+                     "algorithmic_bytes_per_launch": N * BYTES_PER_ENV_STEP},
         "wall_s": float(el_t[1]),
     }
+    tr = pmc_traffic(N, args.dt, args.task)
+    if tr is not None:
+        out["roofline"]["traffic"] = tr[0]
+        out["roofline"]["traffic_source"] = tr[1] + " (bytes per launch)"
     if not args.no_parity:
         try:
             out["max_abs_step_err"] = parity_error(args.dt, args.task)
