@@ -19,3 +19,4 @@ for set in "FETCH_SIZE" "WRITE_SIZE" \
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set --output-format csv -d $D/pmc$i -o run -- python3 bench.py --envs $N --dt $DT --steps 200 --warmup 20 --no-cpu-baseline --no-parity > $D/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $D/pmc$i.log; exit 4; }
 done
 python3 scripts/summarize_prof.py $D $TAG $N $DT
+# profiles/ does not travel back from the box: rerun the summariser locally on gpurun_out/prof_$TAG
