@@ -98,19 +98,29 @@ struct StepArgs {
 #ifndef HG_PARAMS_PTR
 #define HG_PARAMS_PTR 1
 #endif
-#ifndef HG_RK_LOOP
-#define HG_RK_LOOP 0
-#endif
 #if HG_PARAMS_PTR
 using ParamArg = const Params<float>* __restrict__;
 #else
 using ParamArg = const Params<float>;
 #endif
 
+#ifndef HG_MIN_WAVES
+#define HG_MIN_WAVES 1
+#endif
+#ifndef HG_LDS_Y0
+#define HG_LDS_Y0 0
+#endif
+// Diagnostic builds only (timing attribution, never shipped): 1 = all lanes load and store one
+// shared address, 2 = memory only (no wind / RK / reward arithmetic), 3 = compute only (loads from
+// an L2-resident slice, stores behind a never-true test).
+#ifndef HG_DEBUG_PHASE
+#define HG_DEBUG_PHASE 0
+#endif
+
 template <int TASK>
-__global__ __launch_bounds__(kBlock) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
+__global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
-    __shared__ float s_obs[kBlock * HG_N_OBS];
+    __shared__ float s_obs[kBlock * (HG_LDS_Y0 ? 18 : HG_N_OBS)];
 #if HG_PARAMS_PTR
     const Params<float>& P = *Pa;   // model constants: scalar loads from a device copy
 #else
@@ -121,7 +131,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(ParamArg Pa, const Templat
     const int64_t i = blk0 + tid;
     const int64_t n = a.n;
     const bool active = i < n;
-    const int64_t ii = active ? i : 0;   // inactive lanes compute on env 0 and store nothing
+    const int64_t ii = HG_DEBUG_PHASE == 3 ? (i & 255) : ((active && HG_DEBUG_PHASE != 1) ? i : 0);
 
     float hs[18], ws[5], carry[4];
 #pragma unroll
@@ -155,37 +165,45 @@ __global__ __launch_bounds__(kBlock) void step_kernel(ParamArg Pa, const Templat
     // ground height under the committed position (F6), wind step (Heli.step :195-199)
     const hg::Ground<float> h_c = hg::ground_height(P, a.hmap, hs[15], hs[16]);
     float W[3];
+#if HG_DEBUG_PHASE == 2
+    W[0] = ws[0] + eta[0]; W[1] = ws[1] + carry[0]; W[2] = ws[2];
+#else
     hg::wind_step(P, c_tep, ws, carry, eta, W);
+#endif
 
     // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
     const hg::Controls<float> u = hg::controls(P, act.x, act.y, act.z, act.w);
     float k[18], acc[18], st[18], obs[17];
-#if HG_RK_LOOP
+#if HG_DEBUG_PHASE == 2
 #pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] = 0.f; st[c] = hs[c]; }
-#pragma unroll 1
-    for (int stage = 0; stage < 4; ++stage) {
-        hg::dynamics<true>(P, st, u, W, h_c, k, obs);
-        const float w = (stage == 0 || stage == 3) ? 1.f : 2.f;
-        const float cn = stage == 2 ? P.dt : P.half_dt;
+    for (int c = 0; c < 17; ++c) obs[c] = hs[c] + W[c % 3];
 #pragma unroll
-        for (int c = 0; c < 18; ++c) { acc[c] += w * k[c]; st[c] = hs[c] + k[c] * cn; }
-    }
-#pragma unroll
-    for (int c = 0; c < 18; ++c) hs[c] = hs[c] + acc[c] * P.dt6;
+    for (int c = 0; c < 18; ++c) k[c] = hs[c] * u.coll;
 #else
-    hg::dynamics<false>(P, hs, u, W, h_c, k, obs);
+    const hg::Attitude<float> att0 = hg::attitude(hs + 12);
+#if HG_LDS_Y0
+    // y0 of the RK step parked in LDS ([18][256], conflict-free) to cut live VGPRs
+    float* y0 = s_obs;
 #pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
-    hg::dynamics<false>(P, st, u, W, h_c, k, obs);
+    for (int c = 0; c < 18; ++c) y0[c * kBlock + tid] = hs[c];
+#define Y0(c) y0[(c) * kBlock + tid]
+#else
+#define Y0(c) hs[c]
+#endif
+    float e0[3] = {Y0(12), Y0(13), Y0(14)};
+    hg::dynamics<false>(P, hs, u, W, h_c, att0, k, obs);
 #pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
-    hg::dynamics<false>(P, st, u, W, h_c, k, obs);
+    for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = Y0(c) + k[c] * P.half_dt; }
+    hg::dynamics<false>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
 #pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.dt; }
-    hg::dynamics<true>(P, st, u, W, h_c, k, obs);
+    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = Y0(c) + k[c] * P.half_dt; }
+    hg::dynamics<false>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
 #pragma unroll
-    for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
+    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = Y0(c) + k[c] * P.dt; }
+    hg::dynamics<true>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
+#pragma unroll
+    for (int c = 0; c < 18; ++c) hs[c] = Y0(c) + (acc[c] + k[c]) * P.dt6;
+#undef Y0
 #endif
     // step_after (helicopter_dynamics.py:73-77)
     hs[2] = hg::pi_bound(hs[2]);
@@ -210,12 +228,13 @@ __global__ __launch_bounds__(kBlock) void step_kernel(ParamArg Pa, const Templat
     const bool done = term || time_up;
     succ += success_step ? 1 : 0;
 
-    if (active) {
-        a.reward[i] = rew;
-        a.terminated[i] = term;
-        a.truncated[i] = time_up;
+    const int64_t io = HG_DEBUG_PHASE == 1 ? 0 : i;
+    if (active && (HG_DEBUG_PHASE != 3 || (rew == -12345.678f && hs[0] == 1.f))) {
+        a.reward[io] = rew;
+        a.terminated[io] = term;
+        a.truncated[io] = time_up;
         if (a.info)
-            a.info[i] = (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
+            a.info[io] = (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
                                   (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0));
     }
 
@@ -259,26 +278,30 @@ __global__ __launch_bounds__(kBlock) void step_kernel(ParamArg Pa, const Templat
         carry[3] = obs[16];
     }
 
-    if (active) {
+    if (active && (HG_DEBUG_PHASE != 3 || (rew == -12345.678f && hs[0] == 1.f))) {
 #pragma unroll
-        for (int c = 0; c < 18; ++c) a.state[c * n + i] = hs[c];
+        for (int c = 0; c < 18; ++c) a.state[c * n + io] = hs[c];
 #pragma unroll
-        for (int c = 0; c < 5; ++c) a.state[(18 + c) * n + i] = ws[c];
+        for (int c = 0; c < 5; ++c) a.state[(18 + c) * n + io] = ws[c];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) a.state[(23 + c) * n + i] = carry[c];
-        a.counters[i] = step;
-        a.counters[n + i] = succ;
-        a.counters[2 * n + i] = epi;
+        for (int c = 0; c < 4; ++c) a.state[(23 + c) * n + io] = carry[c];
+        a.counters[io] = step;
+        a.counters[n + io] = succ;
+        a.counters[2 * n + io] = epi;
     }
 
     // observations: stage through LDS (stride 17 is bank-conflict free) -> contiguous float4 stores
+#if HG_LDS_Y0
+    __syncthreads();   // the buffer held y0 until here
+#endif
 #pragma unroll
     for (int c = 0; c < 17; ++c) s_obs[tid * 17 + c] = obs[c];
     __syncthreads();
     const int64_t nb = (n - blk0) < kBlock ? (n - blk0) : kBlock;
     const int cnt = (int)nb * 17;
-    float* out = a.obs + blk0 * 17;
+    float* out = a.obs + (HG_DEBUG_PHASE == 1 ? 0 : blk0 * 17);
     const int n4 = cnt >> 2;
+    if (HG_DEBUG_PHASE != 3 || s_obs[tid] == -12345.678f)
     for (int j = tid; j < n4; j += kBlock)
         reinterpret_cast<float4*>(out)[j] = reinterpret_cast<const float4*>(s_obs)[j];
     for (int j = (n4 << 2) + tid; j < cnt; j += kBlock) out[j] = s_obs[j];
@@ -411,7 +434,9 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
     P.mr_VTIP = (R)mr_VT; P.mr_inv_VTIP = (R)(1.0 / mr_VT);
     P.mr_tw75 = (R)(0.75 * a.mr_TWST); P.mr_tw50 = (R)(0.5 * a.mr_TWST);
     P.mr_two3_vtip = (R)(0.66667 * mr_VT);
-    P.mr_gam_dro = (R)(a.mr_A * a.mr_C * pow(a.mr_R, 4) / a.mr_IB * mr_OM / 16 * (1 + 8.0 / 3 * a.mr_E / a.mr_R));
+    const double gam_dro = a.mr_A * a.mr_C * pow(a.mr_R, 4) / a.mr_IB * mr_OM / 16 * (1 + 8.0 / 3 * a.mr_E / a.mr_R);
+    P.mr_gam_dro = (R)gam_dro;
+    P.mr_inv_gam_dro = (R)(1.0 / gam_dro);
     P.mr_kc_num = (R)(0.75 * mr_OM * a.mr_E / a.mr_R);
     P.mr_DL_DB1 = (R)(a.mr_B / 2 * (1.5 * a.mr_IB * a.mr_E / a.mr_R * mr_OM * mr_OM));
     P.mr_DL_DA1_dro = (R)(0.5 * a.mr_A * a.mr_B * a.mr_C * a.mr_R * mr_VT * mr_VT * a.mr_E / 6);
@@ -423,6 +448,7 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
     P.mr_vtip2 = (R)(mr_VT * mr_VT);
     P.mr_2_vtip = (R)(2.0 / mr_VT);
     P.mr_8_asig = (R)(8.0 / mr_ASIG);
+    P.mr_inv_R = (R)(1.0 / a.mr_R);
     const double tr_OM = a.tr_RPM * 2 * M_PI / 60, tr_VT = a.tr_R * tr_OM;
     P.tr_H = (R)tr_H; P.tr_D = (R)tr_D; P.tr_OMEGA = (R)tr_OM;
     P.tr_VTIP = (R)tr_VT; P.tr_inv_VTIP = (R)(1.0 / tr_VT);
@@ -507,7 +533,7 @@ void trim_fcn(const Params<double>& P, const double base[18], const double x[16]
     s[13] = (float)x[11];
     const hg::Controls<double> u = hg::controls(P, x[12], x[13], x[14], x[15]);
     double d[18], ob[17];
-    hg::dynamics<true>(P, s, u, W, h_c, d, ob);
+    hg::dynamics<true>(P, s, u, W, h_c, hg::attitude(s + 12), d, ob);
     y[0] = d[0] / P.mr_VTIP;
     y[1] = d[1] / P.tr_VTIP;
     y[2] = d[4];

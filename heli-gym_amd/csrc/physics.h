@@ -30,6 +30,13 @@ HD double m_fmod(double x, double y) { return fmod(x, y); }
 // [-pi/4, pi/4]; ~1 ulp, ~25 VALU ops for both, no Payne-Hanek slow path (libm sincosf spills a
 // 36-byte scratch table for it).  Larger |x| keeps working with degrading absolute accuracy.
 HD void m_sincos(float x, float* s, float* c) {
+#if defined(HG_HW_SINCOS) && HG_HW_SINCOS && defined(__HIP_DEVICE_COMPILE__)
+    // v_sin_f32 / v_cos_f32 take revolutions
+    const float rv = x * 0.159154943091895336f;
+    *s = __builtin_amdgcn_sinf(rv);
+    *c = __builtin_amdgcn_cosf(rv);
+    return;
+#endif
     const float k = rintf(x * 0.636619772367581343f);
     float r = fmaf(k, -1.57079637050628662109375f, x);
     r = fmaf(k, 4.37113900018624283e-8f, r);
@@ -50,6 +57,45 @@ HD void m_sincos(float x, float* s, float* c) {
     *c = ((q + 1) & 2) ? -cc : cc;
 }
 HD void m_sincos(double x, double* s, double* c) { *s = sin(x); *c = cos(x); }
+
+// sin/cos of the three attitude angles (kinematic.py:4-5,21-22).
+template <typename R>
+struct Attitude {
+    R s[3], c[3];
+};
+
+template <typename R>
+HD Attitude<R> attitude(const R* eul) {
+    Attitude<R> a;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) m_sincos(eul[j], &a.s[j], &a.c[j]);
+    return a;
+}
+
+// Attitude of a RK stage from the committed attitude: sin/cos(e + d) by the angle-addition
+// formulas with short Taylor series for the stage increment d (|d| <= 0.25 rad: truncation
+// < 2e-8); a lane with a larger increment (a tumbling, diverging env) takes the full sincos.
+template <typename R>
+HD Attitude<R> attitude_step(const Attitude<R>& a0, const R* eul0, const R* eul) {
+    Attitude<R> a;
+    bool big = false;
+    R sd[3], cd[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const R d = eul[j] - eul0[j];
+        const R d2 = d * d;
+        big = big || !(m_fabs(d) <= (R)0.25);
+        sd[j] = d * ((R)1 - d2 * (R)(1.0 / 6.0) * ((R)1 - d2 * (R)(1.0 / 20.0)));
+        cd[j] = (R)1 - d2 * (R)0.5 * ((R)1 - d2 * (R)(1.0 / 12.0) * ((R)1 - d2 * (R)(1.0 / 30.0)));
+    }
+    if (big) return attitude(eul);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        a.s[j] = a0.s[j] * cd[j] + a0.c[j] * sd[j];
+        a.c[j] = a0.c[j] * cd[j] - a0.s[j] * sd[j];
+    }
+    return a;
+}
 // x^e for x > 0 (ISA density ratio, Dryden scale lengths)
 HD float m_pow(float x, float e) { return exp2f(e * log2f(x)); }
 HD double m_pow(double x, double e) { return pow(x, e); }
@@ -57,6 +103,23 @@ HD float m_log2(float x) { return log2f(x); }
 HD double m_log2(double x) { return log2(x); }
 HD float m_exp2(float x) { return exp2f(x); }
 HD double m_exp2(double x) { return exp2(x); }
+// Reciprocal: the hardware v_rcp_f32 (1 ulp) on the device instead of a full IEEE division.
+HD float m_rcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+HD double m_rcp(double x) { return 1.0 / x; }
+// True when any lane of the wave has `c` (a uniform skip for rarely taken, costly branches).
+HD bool wave_any(bool c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __any(c);
+#else
+    return c;
+#endif
+}
 template <typename R> HD R m_sign(R x) { return (R)((x > (R)0) - (x < (R)0)); }
 template <typename R> HD R m_max(R a, R b) { return a > b ? a : b; }
 
@@ -81,6 +144,7 @@ struct Params {
     R mr_H, mr_D, mr_IS, mr_K1, mr_R, mr_OMEGA, mr_inv_OMEGA, mr_VTIP, mr_inv_VTIP;
     R mr_tw75, mr_tw50, mr_two3_vtip, mr_gam_dro, mr_kc_num, mr_DL_DB1, mr_DL_DA1_dro, mr_coef;
     R mr_inflow, mr_inv_thr_den, mr_inv_ct_den, mr_prof, mr_vtip2, mr_2_vtip, mr_8_asig;
+    R mr_inv_gam_dro, mr_inv_R;
     // tail rotor
     R tr_H, tr_D, tr_OMEGA, tr_VTIP, tr_inv_VTIP, tr_tw75, tr_tw50, tr_two3_vtip, tr_coef;
     R tr_inflow, tr_inv_thr_den;
@@ -173,25 +237,55 @@ struct Ground {
     HD R zh(R z) const { return ((z + hi) + lo) + delta; }
 };
 
+// The three texels and fractions for a position (split so the kernel can prefetch texels).
 template <typename R>
-HD Ground<R> ground_height(const Params<R>& P, const float2* __restrict__ hmap, R x, R y) {
+struct GroundCell {
+    int mid, north, east;   // texel indices: mid read before the edge decrement (:188), then (:191-192)
+    R fx, fy;               // fractions, with the post-decrement index (:194)
+};
+
+template <typename R>
+HD GroundCell<R> ground_cell(const Params<R>& P, R x, R y) {
     const int rows = P.hm_rows, cols = P.hm_cols;
     int xi, yi;
     R fx, fy;
     map_coord(x * P.hm_sx, rows / 2, rows - 1, &xi, &fx);
     map_coord(y * P.hm_sy, cols / 2, rows - 1, &yi, &fy);   // QUIRK: y clamps to shape[0] (:182-183)
-    const float2 m = hmap[yi * cols + xi];   // read before the edge decrement (:188)
-    if (xi == rows - 1) { xi = rows - 2; fx += (R)1; }   // (:189-190,194) fractions use the
-    if (yi == cols - 1) { yi = cols - 2; fy += (R)1; }   // decremented index
-    const float2 n = hmap[yi * cols + xi + 1];
-    const float2 e = hmap[(yi + 1) * cols + xi];
+    GroundCell<R> c;
+    c.mid = yi * cols + xi;
+    if (xi == rows - 1) { xi = rows - 2; fx += (R)1; }   // (:189-190) edge decrement
+    if (yi == cols - 1) { yi = cols - 2; fy += (R)1; }
+    c.north = yi * cols + xi + 1;
+    c.east = (yi + 1) * cols + xi;
+    c.fx = fx;
+    c.fy = fy;
+    return c;
+}
+
+struct GroundTexels {
+    float2 m, n, e;
+};
+
+template <typename R>
+HD GroundTexels ground_fetch(const float2* __restrict__ hmap, const GroundCell<R>& c) {
+    return GroundTexels{hmap[c.mid], hmap[c.north], hmap[c.east]};
+}
+
+template <typename R>
+HD Ground<R> ground_combine(const GroundTexels& t, const GroundCell<R>& c) {
     Ground<R> g;
-    g.hi = (R)m.x;
-    g.lo = (R)m.y;
-    const R dn = ((R)n.x - (R)m.x) + ((R)n.y - (R)m.y);
-    const R de = ((R)e.x - (R)m.x) + ((R)e.y - (R)m.y);
-    g.delta = dn * fx + de * fy;
+    g.hi = (R)t.m.x;
+    g.lo = (R)t.m.y;
+    const R dn = ((R)t.n.x - (R)t.m.x) + ((R)t.n.y - (R)t.m.y);
+    const R de = ((R)t.e.x - (R)t.m.x) + ((R)t.e.y - (R)t.m.y);
+    g.delta = dn * c.fx + de * c.fy;   // (:194)
     return g;
+}
+
+template <typename R>
+HD Ground<R> ground_height(const Params<R>& P, const float2* __restrict__ hmap, R x, R y) {
+    const GroundCell<R> c = ground_cell(P, x, y);
+    return ground_combine<R>(ground_fetch(hmap, c), c);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -275,17 +369,17 @@ HD WindPar<R> wind_params(const Params<R>& P, const float (*tep)[13], const R ca
         // cos/sin of atan2(ay, ax) without the transcendental (atan2(0,0) = 0)
         const R hyp = m_sqrt(ax * ax + ay * ay);
         const bool z = !(hyp > (R)0);
-        const R ih = z ? (R)0 : (R)1 / hyp;
+        const R ih = z ? (R)0 : m_rcp(hyp);
         ca = z ? (R)1 : ax * ih;
         sa = z ? (R)0 : ay * ih;
     }
-    const R iv = (R)1 / (vel + (R)kEps);
+    const R iv = m_rcp(vel + (R)kEps);
     const R t_u = Lu * iv, t_v = Lv * iv, t_w = Lw * iv;
     WindPar<R> w;
-    w.a_u = (R)1 / t_u;
-    w.a_v = (R)1 / t_v;
+    w.a_u = m_rcp(t_u);
+    w.a_v = m_rcp(t_v);
     w.b_v = (R)0.25 * w.a_v * w.a_v;
-    w.a_w = (R)1 / t_w;
+    w.a_w = m_rcp(t_w);
     w.b_w = (R)0.25 * w.a_w * w.a_w;
     w.K_u = s_u * m_sqrt((R)kTwoDPi * t_u);
     w.K_v = s_v * m_sqrt((R)kTwoDPi * t_v);
@@ -339,22 +433,19 @@ HD void wind_step(const Params<R>& P, const float (*tep)[13], R s[5], const R ca
 // height under the COMMITTED position (F6).  Writes d[18]; with OBS also the 17 observations.
 template <bool OBS, typename R>
 HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>& u, const R W[3],
-                 const Ground<R>& gc, R* __restrict__ d, R* __restrict__ obs) {
+                 const Ground<R>& gc, const Attitude<R>& att, R* __restrict__ d, R* __restrict__ obs) {
     const R vi_mr = s[0], vi_tr = s[1], b0 = s[4], b1 = s[5];
     const R uu = s[6], vv = s[7], ww = s[8], p = s[9], q = s[10], r = s[11];
     const R phi = s[12], th = s[13], psi = s[14];
     const R z = s[17];
 
     // kinematic.py:3-29: B = earth->body DCM, T = pqr->euler rate
-    R s0, c0, s1, c1, s2, c2;
-    m_sincos(phi, &s0, &c0);
-    m_sincos(th, &s1, &c1);
-    m_sincos(psi, &s2, &c2);
+    const R s0 = att.s[0], c0 = att.c[0], s1 = att.s[1], c1 = att.c[1], s2 = att.s[2], c2 = att.c[2];
     const R B00 = c1 * c2, B01 = c1 * s2, B02 = -s1;
     const R s0s1 = s0 * s1, c0s1 = c0 * s1;
     const R B10 = s0s1 * c2 - c0 * s2, B11 = s0s1 * s2 + c0 * c2, B12 = s0 * c1;
     const R B20 = c0s1 * c2 + s0 * s2, B21 = c0s1 * s2 - s0 * c2, B22 = c0 * c1;
-    const R ic1 = (R)1 / c1;
+    const R ic1 = m_rcp(c1);
     const R t1 = s1 * ic1;
     const R phid = p + (s0 * t1) * q + (c0 * t1) * r;
     const R thd = c0 * q - s0 * r;
@@ -372,17 +463,17 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
 
     // ---- main rotor (:203-270)
     const R gam = rho * P.mr_gam_dro;
-    const R igam = (R)1 / gam;
+    const R irho = m_rcp(rho);
+    const R igam = irho * P.mr_inv_gam_dro;
     const R KC = P.mr_kc_num * igam + P.mr_K1;
     const R og = P.mr_OMEGA * igam;
-    const R ITB2_OM = P.mr_OMEGA / ((R)1 + og * og);
+    const R ITB2_OM = P.mr_OMEGA * m_rcp((R)1 + og * og);
     const R ITB = ITB2_OM * og;
     const R DL_DA1 = rho * P.mr_DL_DA1_dro;
     const R vadv2 = ua * ua + va * va;
     const R wr = wa + (b0 - P.mr_IS) * ua - b1 * va;
     const R wb = wr + P.mr_two3_vtip * (u.coll + P.mr_tw75) + vadv2 * P.mr_inv_VTIP * (u.coll + P.mr_tw50);
     const R thr = (wb - vi_mr) * rho * P.mr_coef;
-    const R irho = (R)1 / rho;
     const R dw = wr - vi_mr;
     d[0] = P.mr_inflow * (thr * irho * P.mr_inv_thr_den - vi_mr * m_sqrt(vadv2 + dw * dw));
     const R power_mr = thr * (vi_mr - wr) + rho * P.mr_prof * (P.mr_vtip2 + (R)3 * vadv2);
@@ -413,7 +504,7 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
     // ---- fuselage (:302-320)
     R wa_f = wa - vi_mr;
     wa_f = wa_f > (R)0 ? wa_f + (R)kEps : wa_f;
-    const R d_fw = ((ua / (-wa_f)) * P.fus_dfw_k - P.fus_dfw_c) * P.fus_COR;
+    const R d_fw = ((ua * m_rcp(-wa_f)) * P.fus_dfw_k - P.fus_dfw_c) * P.fus_COR;
     const R rh = (R)0.5 * rho;
     const R X_F = rh * P.fus_XUU * m_fabs(ua) * ua;
     const R Y_F = rh * P.fus_YVV * m_fabs(va) * va;
@@ -422,8 +513,8 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
 
     // ---- horizontal tail (:322-345)
     const R v_dw = m_max(vi_mr - wa, (R)kEps);
-    const R d_dw = ua / v_dw * P.ht_dw_k - P.ht_dw_c;
-    const R eps_ht = (d_dw > (R)0 && d_dw < P.mr_R) ? (R)2 * ((R)1 - d_dw / P.mr_R) : (R)0;
+    const R d_dw = ua * m_rcp(v_dw) * P.ht_dw_k - P.ht_dw_c;
+    const R eps_ht = (d_dw > (R)0 && d_dw < P.mr_R) ? (R)2 * ((R)1 - d_dw * P.mr_inv_R) : (R)0;
     const R wa_ht = wa - eps_ht * vi_mr + P.ht_D * q;
     const R aua = m_fabs(ua);
     R Z_HT;
@@ -447,7 +538,7 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
         const R vta2 = ua * ua + wa_w * wa_w;
         const R qq = P.wn_ZUU * ua * ua + P.wn_ZUW * ua * wa_w;
         Z_WN = m_fabs(wa_w) > (R)0.3 * aua ? rh * P.wn_ZMAX * m_sqrt(vta2) * wa_w : rh * qq;
-        X_WN = -rh / (R)kPi / vta2 * qq * qq;
+        X_WN = -rh * (R)(1.0 / kPi) * m_rcp(vta2) * qq * qq;
     }
     const R power_wn = m_fabs(X_WN * ua);
 
@@ -456,10 +547,19 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
     // K * (pos_z + h) keeps its precision near the ground.
     R Fl0 = 0, Fl1 = 0, Fl2 = 0, Ml0 = 0, Ml1 = 0, Ml2 = 0;
     const R zh = gc.zh(z);
+    R pzh_g[3];
+    bool touch = false;
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        pzh_g[g] = zh + (B02 * P.lg_loc[g][0] + B12 * P.lg_loc[g][1] + B22 * P.lg_loc[g][2]);   // pos_z + h
+        touch = touch || (-pzh_g[g] - P.wl_cg_ft < (R)0);
+    }
+    // contact is rare: the wave skips the spring-damper code unless one of its lanes touches
+    if (wave_any(touch))
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
         const R rx = P.lg_loc[g][0], ry = P.lg_loc[g][1], rz = P.lg_loc[g][2];
-        const R pzh = zh + (B02 * rx + B12 * ry + B22 * rz);   // pos_z + h
+        const R pzh = pzh_g[g];
         if (-pzh - P.wl_cg_ft < (R)0) {                        // -pos_z - (h + WL_CG/12) < 0
             const R cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
             const R vel_z = n2 + (B02 * cx + B12 * cy + B22 * cz);
@@ -528,7 +628,7 @@ template <typename R>
 HD R reward_forward(const Params<R>& P, const R s[18], const R d[18], bool* success) {
     const R vel = m_sqrt(s[6] * s[6] + s[7] * s[7] + s[8] * s[8]);
     const R vn = vel * P.inv_n_v;
-    const R vdn = (s[6] * d[6] + s[7] * d[7] + s[8] * d[8]) / vel * P.inv_n_a;
+    const R vdn = (s[6] * d[6] + s[7] * d[7] + s[8] * d[8]) * m_rcp(vel) * P.inv_n_a;
     const R dn = s[17] * P.inv_n_x, ddn = d[17] * P.inv_n_v;
     R pf = 0, pt = 0;
 #pragma unroll
