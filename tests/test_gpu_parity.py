@@ -276,3 +276,107 @@ def test_single_env_dropin(torch):
     obs, r, term, trunc, info = env.step(np.zeros(4, np.float32))
     assert isinstance(r, float) and isinstance(term, bool) and isinstance(trunc, bool)
     env.close()
+
+
+@pytest.mark.parametrize("n", [1, 63, 65, 257, 1000])
+def test_ragged_batch_sizes(torch, n):
+    """Partial waves / blocks: every env of a ragged batch matches the oracle (obs staging, ballot
+    compaction and stores are bounded by N)."""
+    d = gc.load("0.01")
+    b = gc.single_step_batch(d, "hover")
+    idx = np.arange(n) % len(b["state"])
+    env = make_env(torch, n, "hover", 0.01, autoreset=True)
+    env.set_state(b["state"][idx].astype(np.float32), b["counters"][idx].astype(np.int32))
+    obs, rew, term, trunc, info = env.step(torch.as_tensor(b["actions"][idx].astype(np.float32), device=env.device),
+                                           eta=torch.as_tensor(b["eta"][idx].astype(np.float32), device=env.device))
+    o = obs.cpu().numpy().astype(np.float64)
+    done = (term | trunc).cpu().numpy()
+    tmpl = env.template()["obs"]
+    for j in range(n):
+        ref = tmpl if done[j] else b["obs"][idx[j]]
+        tol = 1e-6 if done[j] else STEP_ABS + STEP_REL * np.abs(ref)
+        assert np.all(gc.step_errors(o[j], ref, gc.OBS_ANGLE_COLS) <= tol + 4 * (b["obs"][idx[j], 16] < 10) * tol), j
+    np.testing.assert_array_equal(np.sort(info["reset_index"].cpu().numpy()), np.nonzero(done)[0])
+    env.close()
+
+
+def test_setters_match_reference_semantics(torch, terrain_u16):
+    """set_trim_cond / set_target / set_max_time (helicopter.py:89-106) through the batched env:
+    the reset state is the re-trimmed one, the reward uses the new target, and `truncated` rises on
+    the step the reference's float time accumulator passes the new max_time."""
+    from heligym_amd import config
+    from oracle.oracle import Oracle
+    N = 256
+    tc = {"gr_alt": 500.0, "ned_vel": [20.0, 0.0, 0.0]}
+    tgt = {"sea_alt": 2200.0, "north_loc": 10.0, "east_loc": -5.0}
+    env = make_env(torch, N, "hover", 0.01, autoreset=False, seed=3)
+    env.set_trim_cond(tc)
+    env.set_target(tgt)
+    env.set_max_time(1.0)
+    obs, _ = env.reset()
+    cfg, _ = config.make_config(task="hover", dt=0.01, trim_cond=tc, target=tgt, max_time=1.0)
+    orc = Oracle(cfg, terrain_u16)
+    tr = orc.trim(tc)
+    o0 = obs.cpu().numpy().astype(np.float64)
+    ref0 = np.array(tr.obs)
+    assert np.all(np.abs(o0 - ref0) <= TRIM_REL * (np.abs(ref0) + 1)), np.abs(o0 - ref0).max(axis=0)
+    act = torch.as_tensor(np.tile(np.array(tr.action, np.float32), (N, 1)), device=env.device)
+    eta = torch.zeros((N, 3), dtype=torch.float32, device=env.device)
+    n_up = gc.time_up_threshold(0.01, 1.0)
+    for k in range(n_up + 2):
+        st, ctr = env.get_state()
+        s = st[0].cpu().numpy().astype(np.float64)
+        prev = np.zeros(17)
+        prev[4:7], prev[16] = s[23:26], s[26]
+        t_acc = sum([0.01] * int(ctr[0, 0]))
+        eo = orc.env_from(s[:18], s[18:23], prev, np.zeros(18), t_acc, 0.0, state_f32=(k == 0))
+        oo = orc.step(eo, np.array(tr.action, np.float32), np.zeros(3))
+        obs, rew, term, trunc, info = env.step(act, eta=eta)
+        assert abs(float(rew[0]) - oo.reward_hover) <= 1e-4 * (1 + abs(oo.reward_hover)), (k, float(rew[0]),
+                                                                                          oo.reward_hover)
+        assert bool(trunc[0]) == (k + 1 >= n_up) == bool(info["time_up"][0]), k
+        assert not bool(term[0])
+    env.close()
+
+
+def test_graph_capture_replays_like_eager(torch):
+    """hg_step on torch's current stream is hipGraph-capturable; a replay equals eager stepping."""
+    N, K = 512, 20
+    outs = []
+    for use_graph in (False, True):
+        env = make_env(torch, N, "hover", 0.01, autoreset=True, seed=9)
+        env.reset()
+        bank = torch.empty((K, N, 4), dtype=torch.float32, device=env.device)
+        for k in range(K):
+            env.random_actions(bank[k], seed=4, step=k)
+        torch.cuda.synchronize()
+        if use_graph:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for k in range(K):
+                    env.step_async(bank[k], with_reset_info=False)
+            env.reset()                      # capture does not execute: start from the reset state
+            g.replay()
+        else:
+            env.reset()                      # same episode index (it keys the noise) as the graph run
+            for k in range(K):
+                env.step_async(bank[k], with_reset_info=False)
+        torch.cuda.synchronize()
+        st, ctr = env.get_state()
+        outs.append((env.obs.cpu().numpy().copy(), st.cpu().numpy().copy(), ctr.cpu().numpy().copy()))
+        env.close()
+    for a, b in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_heli_task_reward_is_zero(torch):
+    env = make_env(torch, 128, "heli", 0.02, autoreset=True)
+    env.reset()
+    act = torch.empty((128, 4), dtype=torch.float32, device=env.device)
+    for k in range(5):
+        env.random_actions(act, seed=1, step=k)
+        obs, rew, *_ = env.step(act)
+        assert float(rew.abs().max()) == 0.0       # helicopter.py:242-243
+    env.close()
