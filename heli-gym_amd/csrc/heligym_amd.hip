@@ -50,8 +50,6 @@ constexpr int kBlock = 256;
 constexpr int kStateCols = HG_STATE_COLS;
 constexpr int kCtrCols = HG_COUNTER_COLS;
 
-__constant__ float c_tep[8][13] = HG_TEP_TABLE;
-const float h_tep[8][13] = HG_TEP_TABLE;
 
 // ------------------------------------------------------------------------------ Philox4x32-10
 struct U4 {
@@ -107,20 +105,67 @@ using ParamArg = const Params<float>;
 #ifndef HG_MIN_WAVES
 #define HG_MIN_WAVES 1
 #endif
-#ifndef HG_LDS_Y0
-#define HG_LDS_Y0 0
+
+constexpr int kTplFloats = (int)(sizeof(Template<float>) / sizeof(float));
+static_assert(kTplFloats <= 64, "reset template must fit one float per lane");
+__device__ __forceinline__ float lane_value(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Output stores.  NT = non-temporal for the dword-and-wider columns (the byte flags stay plain):
+// used when the whole batch is resident at once (<= one wave per SIMD), where the step is latency
+// bound and streaming the outputs shortens the end-of-kernel write-back; with more waves than
+// SIMDs the plain write-back path is faster.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+template <bool NT, typename T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+    if constexpr (NT && sizeof(T) >= 4) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <bool NT>
+__device__ __forceinline__ void st_out4(float* p, const float* s) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(s);
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+    else *reinterpret_cast<f32x4*>(p) = v;
+}
+
+// Per-lane access at a small byte offset from a uniform base (SGPR-base global load / store).
+template <typename T>
+__device__ __forceinline__ T ld_lane(const T* __restrict__ base, uint32_t idx) {
+    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + idx * (uint32_t)sizeof(T));
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st_lane(T* base, uint32_t idx, T v) {
+    st_out<NT>(reinterpret_cast<T*>(reinterpret_cast<char*>(base) + idx * (uint32_t)sizeof(T)), v);
+}
+
+// Diagnostic build only: per-wave phase timestamps (s_memtime) of one launch, for latency
+// attribution; lane 0 of each of the first HG_TIMING_WAVES waves records them.
+#ifndef HG_TIMING
+#define HG_TIMING 0
 #endif
-// Diagnostic builds only (timing attribution, never shipped): 1 = all lanes load and store one
-// shared address, 2 = memory only (no wind / RK / reward arithmetic), 3 = compute only (loads from
-// an L2-resident slice, stores behind a never-true test).
-#ifndef HG_DEBUG_PHASE
-#define HG_DEBUG_PHASE 0
+#if HG_TIMING
+#define HG_TIMING_WAVES 2048
+#define HG_TIMING_SLOTS 16
+__device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
+#define TSTAMP(j, ...)                                                                          \
+    do {                                                                                        \
+        asm volatile("" ::__VA_ARGS__);                                                         \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+        const int w_ = (int)(i >> 6);                                                           \
+        if ((tid & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;                      \
+    } while (0)
+#else
+#define TSTAMP(j, ...) do { } while (0)
 #endif
 
-template <int TASK>
+// TASK: reward / success of the task; ETA: noise injected by the caller (else in-kernel Philox);
+// NT: streaming output stores (see st_out).  All compile-time, so the hot kernel has no
+// data-independent branches to merge around.
+template <int TASK, bool ETA, bool NT>
 __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
-    __shared__ float s_obs[kBlock * (HG_LDS_Y0 ? 18 : HG_N_OBS)];
+    __shared__ float s_obs[kBlock * HG_N_OBS];
 #if HG_PARAMS_PTR
     const Params<float>& P = *Pa;   // model constants: scalar loads from a device copy
 #else
@@ -131,26 +176,51 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     const int64_t i = blk0 + tid;
     const int64_t n = a.n;
     const bool active = i < n;
-    const int64_t ii = HG_DEBUG_PHASE == 3 ? (i & 255) : ((active && HG_DEBUG_PHASE != 1) ? i : 0);
+    // Addressing: uniform (SGPR) bases at this block's first env plus a small per-lane byte offset,
+    // so loads and stores use the SGPR-base form with no per-access 64-bit address arithmetic.
+    // Lanes past the end of a ragged last block read env blk0 and store nothing.
+    const uint32_t lo = (uint32_t)(active ? tid : 0);
+#define COL(ptr, c) ((ptr) + (int64_t)(c) * n)
+    // (the block bases are re-derived behind an opaque copy for the stores, so the compiler does
+    // not keep ~30 column addresses live across the whole step)
+    float* st_b = a.state + blk0;
+    int32_t* ct_b = a.counters + blk0;
 
+#if HG_TIMING
+    if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][15] = __builtin_amdgcn_s_memrealtime();
+#endif
+    TSTAMP(0, "v"(tid));
+    // Loads in the order they are needed: position (-> terrain texel address), counters (-> noise
+    // key), then the rest; the reset template is spread one float per lane (read back with
+    // readlane by resetting lanes) so a reset adds no memory round trip at the end of the step.
     float hs[18], ws[5], carry[4];
+    hs[15] = ld_lane(COL(st_b, 15), lo);
+    hs[16] = ld_lane(COL(st_b, 16), lo);
+    int32_t step = ld_lane(COL(ct_b, 0), lo), succ = ld_lane(COL(ct_b, 1), lo),
+            epi = ld_lane(COL(ct_b, 2), lo);
 #pragma unroll
-    for (int c = 0; c < 18; ++c) hs[c] = a.state[c * n + ii];
+    for (int c = 0; c < 18; ++c)
+        if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lo);
 #pragma unroll
-    for (int c = 0; c < 5; ++c) ws[c] = a.state[(18 + c) * n + ii];
+    for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lo);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) carry[c] = a.state[(23 + c) * n + ii];
-    int32_t step = a.counters[ii], succ = a.counters[n + ii], epi = a.counters[2 * n + ii];
-    const float4 act = reinterpret_cast<const float4*>(a.actions)[ii];
+    for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lo);
+    const float4 act = ld_lane(reinterpret_cast<const float4*>(a.actions) + blk0, lo);
+    const int lane = tid & 63;
+    // terrain texels under the committed position (F6): issued now, combined after the wind step
+    const hg::GroundCell<float> cell_c = hg::ground_cell(P, hs[15], hs[16]);
+    const hg::GroundTexels tex_c = hg::ground_fetch(a.hmap, cell_c);
 
+    TSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(epi), "v"(carry[3]), "v"(ws[4]));
     // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
     float eta[3];
-    if (a.eta) {
-        eta[0] = a.eta[3 * ii + 0];
-        eta[1] = a.eta[3 * ii + 1];
-        eta[2] = a.eta[3 * ii + 2];
+    if (ETA) {
+        const float* eb = a.eta + 3 * blk0;
+        eta[0] = ld_lane(eb + 0, 3 * lo);
+        eta[1] = ld_lane(eb + 1, 3 * lo);
+        eta[2] = ld_lane(eb + 2, 3 * lo);
     } else {
-        const uint64_t gid = (uint64_t)(a.env_offset + ii);
+        const uint64_t gid = (uint64_t)(a.env_offset + blk0 + lo);
         const U4 r = philox(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)epi},
                             (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
         float sn, cs;
@@ -163,48 +233,37 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     }
 
     // ground height under the committed position (F6), wind step (Heli.step :195-199)
-    const hg::Ground<float> h_c = hg::ground_height(P, a.hmap, hs[15], hs[16]);
+    TSTAMP(2, "v"(eta[2]), "v"(eta[0]));
     float W[3];
-#if HG_DEBUG_PHASE == 2
-    W[0] = ws[0] + eta[0]; W[1] = ws[1] + carry[0]; W[2] = ws[2];
-#else
-    hg::wind_step(P, c_tep, ws, carry, eta, W);
-#endif
+    hg::wind_step(P, ws, carry, eta, W);
+    TSTAMP(3, "v"(W[2]), "v"(W[0]));
+    const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
 
+    TSTAMP(4, "v"(h_c.delta), "v"(h_c.hi));
     // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
     const hg::Controls<float> u = hg::controls(P, act.x, act.y, act.z, act.w);
     float k[18], acc[18], st[18], obs[17];
-#if HG_DEBUG_PHASE == 2
-#pragma unroll
-    for (int c = 0; c < 17; ++c) obs[c] = hs[c] + W[c % 3];
-#pragma unroll
-    for (int c = 0; c < 18; ++c) k[c] = hs[c] * u.coll;
-#else
     const hg::Attitude<float> att0 = hg::attitude(hs + 12);
-#if HG_LDS_Y0
-    // y0 of the RK step parked in LDS ([18][256], conflict-free) to cut live VGPRs
-    float* y0 = s_obs;
-#pragma unroll
-    for (int c = 0; c < 18; ++c) y0[c * kBlock + tid] = hs[c];
-#define Y0(c) y0[(c) * kBlock + tid]
-#else
-#define Y0(c) hs[c]
-#endif
-    float e0[3] = {Y0(12), Y0(13), Y0(14)};
+    float e0[3] = {hs[12], hs[13], hs[14]};
     hg::dynamics<false>(P, hs, u, W, h_c, att0, k, obs);
+    TSTAMP(5, "v"(k[8]), "v"(k[11]));
 #pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = Y0(c) + k[c] * P.half_dt; }
+    for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
     hg::dynamics<false>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
+    TSTAMP(6, "v"(k[8]), "v"(k[11]));
 #pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = Y0(c) + k[c] * P.half_dt; }
+    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
     hg::dynamics<false>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
+    TSTAMP(7, "v"(k[8]), "v"(k[11]));
 #pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = Y0(c) + k[c] * P.dt; }
+    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.dt; }
     hg::dynamics<true>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
 #pragma unroll
-    for (int c = 0; c < 18; ++c) hs[c] = Y0(c) + (acc[c] + k[c]) * P.dt6;
-#undef Y0
-#endif
+    for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
+    TSTAMP(8, "v"(hs[8]), "v"(hs[11]), "v"(obs[16]));
+    // reset template (heli[18] | carry[4] | obs[17]) one float per lane, fetched now so that its
+    // latency hides behind the reward / flag work and a reset costs no round trip at the end
+    const float tpl = lane < kTplFloats ? reinterpret_cast<const float*>(Tp)[lane] : 0.f;
     // step_after (helicopter_dynamics.py:73-77)
     hs[2] = hg::pi_bound(hs[2]);
     hs[3] = hg::pi_bound(hs[3]);
@@ -222,20 +281,20 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
     step += 1;
     const bool failed = hg::is_failed(P, hs, k, h_post);
+    TSTAMP(9, "v"(rew), "v"((int)failed));
     const bool successed = succ >= P.success_steps;   // successed_time before this step's add
     const bool time_up = step >= P.time_up_steps;
     const bool term = failed || successed;
     const bool done = term || time_up;
     succ += success_step ? 1 : 0;
 
-    const int64_t io = HG_DEBUG_PHASE == 1 ? 0 : i;
-    if (active && (HG_DEBUG_PHASE != 3 || (rew == -12345.678f && hs[0] == 1.f))) {
-        a.reward[io] = rew;
-        a.terminated[io] = term;
-        a.truncated[io] = time_up;
+    if (active) {
+        st_lane<NT>(a.reward + blk0, (uint32_t)tid, rew);
+        st_lane<NT>(a.terminated + blk0, (uint32_t)tid, (uint8_t)term);
+        st_lane<NT>(a.truncated + blk0, (uint32_t)tid, (uint8_t)time_up);
         if (a.info)
-            a.info[io] = (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
-                                  (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0));
+            st_lane<NT>(a.info + blk0, (uint32_t)tid, (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
+                                  (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0)));
     }
 
     // same-step auto-reset with a wave-ballot compaction of the finished envs
@@ -243,7 +302,6 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     if (P.autoreset && a.reset_count) {
         const unsigned long long mask = __ballot(do_reset);
         if (mask) {
-            const int lane = tid & 63;
             const int leader = __ffsll((long long)mask) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(a.reset_count, __popcll(mask));
@@ -259,15 +317,15 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
         }
     }
     if (do_reset) {
-        const Template<float>& T = *Tp;   // reset template in HBM (read only by resetting lanes)
+        // Template<float> = heli[18] | carry[4] | obs[17], float c held by lane c
 #pragma unroll
-        for (int c = 0; c < 18; ++c) hs[c] = T.heli[c];
+        for (int c = 0; c < 18; ++c) hs[c] = lane_value(tpl, c);
 #pragma unroll
         for (int c = 0; c < 5; ++c) ws[c] = 0.f;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) carry[c] = T.carry[c];
+        for (int c = 0; c < 4; ++c) carry[c] = lane_value(tpl, 18 + c);
 #pragma unroll
-        for (int c = 0; c < 17; ++c) obs[c] = T.obs[c];
+        for (int c = 0; c < 17; ++c) obs[c] = lane_value(tpl, 22 + c);
         step = 0;
         succ = 0;
         epi += 1;
@@ -278,33 +336,44 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
         carry[3] = obs[16];
     }
 
-    if (active && (HG_DEBUG_PHASE != 3 || (rew == -12345.678f && hs[0] == 1.f))) {
+    TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
+    st_b = a.state + blk0;
+    ct_b = a.counters + blk0;
+    asm volatile("" : "+s"(st_b), "+s"(ct_b));
+    if (active) {
 #pragma unroll
-        for (int c = 0; c < 18; ++c) a.state[c * n + io] = hs[c];
+        for (int c = 0; c < 18; ++c) st_lane<NT>(COL(st_b, c), (uint32_t)tid, hs[c]);
 #pragma unroll
-        for (int c = 0; c < 5; ++c) a.state[(18 + c) * n + io] = ws[c];
+        for (int c = 0; c < 5; ++c) st_lane<NT>(COL(st_b, 18 + c), (uint32_t)tid, ws[c]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) a.state[(23 + c) * n + io] = carry[c];
-        a.counters[io] = step;
-        a.counters[n + io] = succ;
-        a.counters[2 * n + io] = epi;
+        for (int c = 0; c < 4; ++c) st_lane<NT>(COL(st_b, 23 + c), (uint32_t)tid, carry[c]);
+        st_lane<NT>(COL(ct_b, 0), (uint32_t)tid, step);
+        st_lane<NT>(COL(ct_b, 1), (uint32_t)tid, succ);
+        st_lane<NT>(COL(ct_b, 2), (uint32_t)tid, epi);
     }
 
+    TSTAMP(10, "v"(hs[0]));
     // observations: stage through LDS (stride 17 is bank-conflict free) -> contiguous float4 stores
-#if HG_LDS_Y0
-    __syncthreads();   // the buffer held y0 until here
-#endif
+    // observations: each wave stages its 64 rows in its own LDS slice (stride 17 is bank-conflict
+    // free) and writes them back as contiguous float4, with no block-wide barrier
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
+    float* w_obs = s_obs + wv * 64 * HG_N_OBS;
 #pragma unroll
-    for (int c = 0; c < 17; ++c) s_obs[tid * 17 + c] = obs[c];
-    __syncthreads();
-    const int64_t nb = (n - blk0) < kBlock ? (n - blk0) : kBlock;
-    const int cnt = (int)nb * 17;
-    float* out = a.obs + (HG_DEBUG_PHASE == 1 ? 0 : blk0 * 17);
+    for (int c = 0; c < 17; ++c) w_obs[lane * 17 + c] = obs[c];
+    __builtin_amdgcn_wave_barrier();
+    const int64_t w0 = blk0 + wv * 64;
+    const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
+    const int cnt = nw > 0 ? nw * 17 : 0;
+    float* out = a.obs + w0 * 17;
     const int n4 = cnt >> 2;
-    if (HG_DEBUG_PHASE != 3 || s_obs[tid] == -12345.678f)
-    for (int j = tid; j < n4; j += kBlock)
-        reinterpret_cast<float4*>(out)[j] = reinterpret_cast<const float4*>(s_obs)[j];
-    for (int j = (n4 << 2) + tid; j < cnt; j += kBlock) out[j] = s_obs[j];
+    for (int j = lane; j < n4; j += 64) st_out4<NT>(out + 4 * j, w_obs + 4 * j);
+    for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
+    TSTAMP(11, "v"(tid));
+#if HG_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    TSTAMP(12, "v"(tid));
+    if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][14] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 // Heli.reset for masked envs (helicopter.py:208-217)
@@ -470,6 +539,10 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
                               {-(a.lg_FS_MN - a.FS_CG), -a.lg_BL_MN, -(a.lg_WL - a.WL_CG)}};
     for (int g = 0; g < 3; ++g)
         for (int j = 0; j < 3; ++j) P.lg_loc[g][j] = (R)(loc[g][j] / 12.0);   // :123-126
+    double reach = 0;
+    for (int g = 0; g < 3; ++g)
+        reach = fmax(reach, sqrt(loc[g][0] * loc[g][0] + loc[g][1] * loc[g][1] + loc[g][2] * loc[g][2]) / 12.0);
+    P.lg_reach = (R)(reach * 1.001 + 1e-3);
     // inertia and inverse (:151-154)
     const double Ix = a.IX, Iy = a.IY, Iz = a.IZ, Ixz = -a.IXZ;
     const double det = Ix * Iz - Ixz * Ixz;
@@ -496,6 +569,7 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
     P.w20 = (R)w20;
     P.sigma_low = (R)(0.1 * w20);
     P.turb_level = (R)a.env_TURB_LVL;
+    hg::tep_row_values(P.turb_level, P.tep_row);
     P.eta_norm = (R)(1.0 / sqrt(dt));
     // task (helicopter.py:63-68, helicopter_with_tasks.py:33, 87-88)
     const double n_t = sqrt(2 * a.mr_R / a.env_GRAV), n_x = 2 * a.mr_R, n_v = sqrt(2 * a.mr_R * a.env_GRAV);
@@ -666,6 +740,7 @@ struct hg_env {
     Template<float>* tmpl_dev = nullptr;
     Params<float>* params_dev = nullptr;
     hg_trim_result trim;
+    int64_t resident_envs = 0;   // one wave per SIMD on this device: 64 lanes x 4 SIMDs x CUs
 };
 
 // Upload the fp32 model constants the step kernel reads (after create and every setter).
@@ -705,6 +780,11 @@ static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) 
 #endif
 
 extern "C" {
+#if HG_TIMING
+int hg_debug_timing(void* dst, int64_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_timing), (size_t)bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int32_t hg_abi_version(void) { return HG_ABI_VERSION; }
 
@@ -787,6 +867,11 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
         return fail(HG_E_HIP, std::string(what) + ": " + hipGetErrorString(err));
     };
     hipError_t err;
+    int dev = 0, cus = 0;
+    if ((err = hipGetDevice(&dev)) != hipSuccess) return cleanup(err, "hipGetDevice");
+    if ((err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+        return cleanup(err, "hipDeviceGetAttribute");
+    e->resident_envs = (int64_t)cus * 4 * 64;
     if ((err = hipMalloc(&e->hmap, sizeof(float2) * rows * cols)) != hipSuccess) return cleanup(err, "hipMalloc terrain");
     if ((err = hipMalloc(&e->state, sizeof(float) * kStateCols * num_envs)) != hipSuccess) return cleanup(err, "hipMalloc state");
     if ((err = hipMalloc(&e->counters, sizeof(int32_t) * kCtrCols * num_envs)) != hipSuccess) return cleanup(err, "hipMalloc counters");
@@ -886,17 +971,23 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;
     const dim3 grid(grid_for(e->n)), block(kBlock);
+#define HG_LAUNCH_STEP_NT(T, NT)                                                                           \
+    do {                                                                                                   \
+        if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+        else hipLaunchKernelGGL((step_kernel<T, false, NT>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+    } while (0)
+#define HG_LAUNCH_STEP(T)                                   \
+    do {                                                    \
+        if (e->n <= e->resident_envs) HG_LAUNCH_STEP_NT(T, true); \
+        else HG_LAUNCH_STEP_NT(T, false);                   \
+    } while (0)
     switch (e->cfg.task) {
-        case HG_TASK_HOVER:
-            hipLaunchKernelGGL(step_kernel<HG_TASK_HOVER>, grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);
-            break;
-        case HG_TASK_FORWARD_FLIGHT:
-            hipLaunchKernelGGL(step_kernel<HG_TASK_FORWARD_FLIGHT>, grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);
-            break;
-        default:
-            hipLaunchKernelGGL(step_kernel<HG_TASK_HELI>, grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);
-            break;
+        case HG_TASK_HOVER: HG_LAUNCH_STEP(HG_TASK_HOVER); break;
+        case HG_TASK_FORWARD_FLIGHT: HG_LAUNCH_STEP(HG_TASK_FORWARD_FLIGHT); break;
+        default: HG_LAUNCH_STEP(HG_TASK_HELI); break;
     }
+#undef HG_LAUNCH_STEP_NT
+#undef HG_LAUNCH_STEP
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }

@@ -156,7 +156,7 @@ struct Params {
     R wn_ZUU, wn_ZUW, wn_ZMAX;
     int32_t wn_on;
     // landing gear
-    R lg_K, lg_C, lg_loc[3][3];
+    R lg_K, lg_C, lg_loc[3][3], lg_reach;   // lg_reach: max |r_g| plus a rounding margin
     // inertia: I = [[Ixx,0,Ixz],[0,Iyy,0],[Ixz,0,Izz]] (Ixz = -IXZ), and its inverse
     R Ixx, Iyy, Izz, Ixz, Ji00, Ji02, Ji11, Ji20, Ji22;
     // terrain (helicopter_dynamics.py:167-195)
@@ -164,6 +164,7 @@ struct Params {
     int32_t hm_rows, hm_cols;
     // Dryden wind (wind_dynamics.py:21-83)
     R wm[3], wind_dir_cos, wind_dir_sin, w20, sigma_low, turb_level, eta_norm;
+    R tep_row[13];   // TEP table interpolated at turb_level, per altitude key (tep_row_values)
     // task (helicopter.py:63-68, helicopter_with_tasks.py)
     R n_t, n_t2, inv_n_x, inv_n_v, inv_n_a, tgt_n[3], vel_tgt_n, dwn_tgt_n;
     R fail_zdot, fail_ang;
@@ -313,28 +314,48 @@ struct WindPar {
      {6.f, 15.6f, 17.6f, 23.0f, 23.6f, 22.1f, 20.0f, 16.0f, 15.1f, 12.1f, 7.9f, 6.2f, 5.1f},      \
      {7.f, 18.7f, 21.5f, 28.4f, 30.2f, 30.7f, 31.0f, 25.2f, 23.1f, 17.5f, 10.7f, 8.4f, 7.2f}}
 
+constexpr float kTep[8][13] = HG_TEP_TABLE;
+
 // lookup.py:146-183 (get_value_2D) on the 7x12 TEP table: row key = turbulence level, column
 // key = ground altitude; clamped linear interpolation, no extrapolation.  The reference caches
 // the last bracket index, which only changes where its search starts, not the bracket found.
+// Split in two: the row interpolation depends only on the (per-model) turbulence level and is
+// done once on the host into Params::tep_row; the per-env column bracket is found by comparing
+// against the literal altitude keys (no dependent table loads on the device).
 template <typename R>
-HD R tep_lookup(const float (*tep)[13], R rowKey, R colKey) {
-    int r = 2, c = 2;
-    for (int k = 0; k < 5; ++k) r += (r < 7 && (R)tep[r][0] < rowKey) ? 1 : 0;
-    for (int k = 0; k < 10; ++k) c += (c < 12 && (R)tep[0][c] < colKey) ? 1 : 0;
-    const R r0 = (R)tep[r - 1][0], r1 = (R)tep[r][0], k0 = (R)tep[0][c - 1], k1 = (R)tep[0][c];
+void tep_row_values(R rowKey, R out[13]) {
+    int r = 2;
+    for (int k = 0; k < 5; ++k) r += (r < 7 && (R)kTep[r][0] < rowKey) ? 1 : 0;
+    const R r0 = (R)kTep[r - 1][0], r1 = (R)kTep[r][0];
     R rF = (rowKey - r0) / (r1 - r0);
-    R cF = (colKey - k0) / (k1 - k0);
     rF = rF > (R)1 ? (R)1 : (rF < (R)0 ? (R)0 : rF);
+    for (int c = 0; c < 13; ++c) {
+        const R a0 = (R)kTep[r - 1][c], a1 = (R)kTep[r][c];
+        out[c] = rF * (a1 - a0) + a0;
+    }
+}
+
+template <typename R>
+HD R tep_lookup(const R* __restrict__ row, R colKey) {
+    // bracket c = 2 + #{j in [2, 12): key_j < colKey} (keys increase); k0/k1 and the row values at
+    // c - 1 and c by compare-and-select
+    R k0 = (R)kTep[0][1], k1 = (R)kTep[0][2], v0 = row[1], v1 = row[2];
+#pragma unroll
+    for (int j = 2; j < 12; ++j) {
+        const bool up = (R)kTep[0][j] < colKey;
+        k0 = up ? (R)kTep[0][j] : k0;
+        k1 = up ? (R)kTep[0][j + 1] : k1;
+        v0 = up ? row[j] : v0;
+        v1 = up ? row[j + 1] : v1;
+    }
+    R cF = (colKey - k0) / (k1 - k0);
     cF = cF > (R)1 ? (R)1 : (cF < (R)0 ? (R)0 : cF);
-    const R a0 = (R)tep[r - 1][c - 1], a1 = (R)tep[r][c - 1], b0 = (R)tep[r - 1][c], b1 = (R)tep[r][c];
-    const R c1 = rF * (a1 - a0) + a0;
-    const R c2 = rF * (b1 - b0) + b0;
-    return c1 + cF * (c2 - c1);
+    return v0 + cF * (v1 - v0);
 }
 
 // wind_dynamics.py:54-83 (_calc_params) folded with the stage-invariant part of :92-99, 112-118.
 template <typename R>
-HD WindPar<R> wind_params(const Params<R>& P, const float (*tep)[13], const R carry[4]) {
+HD WindPar<R> wind_params(const Params<R>& P, const R carry[4]) {
     const R vx = carry[0] + P.wm[0], vy = carry[1] + P.wm[1], vz = carry[2] + P.wm[2];
     const R vel = m_sqrt(vx * vx + vy * vy + vz * vz);
     R h = carry[3];
@@ -354,14 +375,14 @@ HD WindPar<R> wind_params(const Params<R>& P, const float (*tep)[13], const R ca
         R ax, ay;
         if (h >= (R)2000) {                   // high altitude
             Lu = (R)1750; Lv = (R)875; Lw = (R)875;
-            s_u = tep_lookup(tep, P.turb_level, h);
+            s_u = tep_lookup(P.tep_row, h);
             ax = vx; ay = vy;
         } else {                              // medium: blend of the two (QUIRK: Lw = Lu, :76)
             const R r = (h - (R)1000) * (R)0.001;
             Lu = (R)1000 + r * (R)750;
             Lv = (R)0.5 * Lu;
             Lw = Lu;
-            s_u = P.sigma_low + r * (tep_lookup(tep, P.turb_level, h) - P.sigma_low);
+            s_u = P.sigma_low + r * (tep_lookup(P.tep_row, h) - P.sigma_low);
             ax = vx * r + P.wm[0] * ((R)1 - r);
             ay = vy * r + P.wm[1] * ((R)1 - r);
         }
@@ -403,9 +424,9 @@ HD void wind_f(const WindPar<R>& w, const R eta[3], const R s[5], R d[5]) {
 // derivative object is aliased across the RK stages, so the update is s += dt * k4; the stage
 // inputs are still formed from k1..k3.  Wind output from the stage-4 input state.
 template <typename R>
-HD void wind_step(const Params<R>& P, const float (*tep)[13], R s[5], const R carry[4], const R eta[3],
+HD void wind_step(const Params<R>& P, R s[5], const R carry[4], const R eta[3],
                   R W[3]) {
-    const WindPar<R> w = wind_params(P, tep, carry);
+    const WindPar<R> w = wind_params(P, carry);
     R k[5], st[5];
     wind_f(w, eta, s, k);
 #pragma unroll
@@ -547,19 +568,14 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
     // K * (pos_z + h) keeps its precision near the ground.
     R Fl0 = 0, Fl1 = 0, Fl2 = 0, Ml0 = 0, Ml1 = 0, Ml2 = 0;
     const R zh = gc.zh(z);
-    R pzh_g[3];
-    bool touch = false;
-#pragma unroll
-    for (int g = 0; g < 3; ++g) {
-        pzh_g[g] = zh + (B02 * P.lg_loc[g][0] + B12 * P.lg_loc[g][1] + B22 * P.lg_loc[g][2]);   // pos_z + h
-        touch = touch || (-pzh_g[g] - P.wl_cg_ft < (R)0);
-    }
-    // contact is rare: the wave skips the spring-damper code unless one of its lanes touches
-    if (wave_any(touch))
+    // Contact is rare.  A gear point's pos_z + h is zh + (B^T r_g)_z <= zh + |r_g|, so no point can
+    // touch while zh + max|r_g| <= -WL_CG/12 (lg_reach carries a rounding margin): the wave skips
+    // the per-point tests and the spring-damper code unless one of its lanes is that close.
+    if (wave_any(zh + P.lg_reach > -P.wl_cg_ft))
 #pragma unroll
     for (int g = 0; g < 3; ++g) {
         const R rx = P.lg_loc[g][0], ry = P.lg_loc[g][1], rz = P.lg_loc[g][2];
-        const R pzh = pzh_g[g];
+        const R pzh = zh + (B02 * rx + B12 * ry + B22 * rz);   // pos_z + h
         if (-pzh - P.wl_cg_ft < (R)0) {                        // -pos_z - (h + WL_CG/12) < 0
             const R cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
             const R vel_z = n2 + (B02 * cx + B12 * cy + B22 * cz);

@@ -1,0 +1,59 @@
+"""Latency attribution of one step launch with a HG_TIMING=1 diagnostic build of the library
+(HELIGYM_AMD_LIB=<that .so>): per-wave s_memtime stamps at phase boundaries -> median / p90 of each
+phase over the recorded waves, plus the spread of wave start / end times.  Diagnostic only."""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "heli-gym_amd"))
+
+PHASES = ["state loads", "philox", "ground h_c", "wind step", "RK stage 1", "RK stage 2", "RK stage 3",
+          "RK stage 4", "reward+flags+ground", "flag stores+reset", "state stores", "obs LDS+stores",
+          "store drain"]
+ORDER = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 13, 10, 11, 12]   # stamp slots in program order
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--warm", type=int, default=300)
+    ap.add_argument("--dt", type=float, default=0.01)
+    args = ap.parse_args()
+    import torch
+    from heligym_amd import HeliVecEnv
+    env = HeliVecEnv(args.envs, task="hover", dt=args.dt, seed=0)
+    env.reset()
+    act = torch.empty((args.envs, 4), dtype=torch.float32, device=env.device)
+    for k in range(args.warm):
+        env.random_actions(act, seed=1, step=k)
+        env.step_async(act, with_reset_info=False)
+    torch.cuda.synchronize()
+    buf = np.zeros((2048, 16), dtype=np.uint64)
+    fn = env.lib.hg_debug_timing
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    assert fn(buf.ctypes.data, buf.nbytes) == 0
+    nw = min(2048, args.envs // 64)
+    t = buf[:nw, ORDER].astype(np.int64)
+    rt = buf[:nw, 14:16].astype(np.int64)        # [end, start] s_memrealtime (100 MHz)
+    span_cyc = (t[:, -1] - t[:, 0]).astype(np.float64)
+    span_ns = (rt[:, 0] - rt[:, 1]) * 10.0
+    ghz = np.median(span_cyc / np.maximum(span_ns, 1))
+    print(f"waves {nw}; memtime clock ~{ghz:.2f} GHz (from realtime); wave life median "
+          f"{np.median(span_ns)/1e3:.2f} us p90 {np.percentile(span_ns, 90)/1e3:.2f} us")
+    starts = (rt[:, 1] - rt[:, 1].min()) * 10.0
+    ends = (rt[:, 0] - rt[:, 1].min()) * 10.0
+    print(f"wave start spread: p50 {np.median(starts)/1e3:.2f} us p90 {np.percentile(starts, 90)/1e3:.2f} "
+          f"max {starts.max()/1e3:.2f} us; last wave end {ends.max()/1e3:.2f} us")
+    d = np.diff(t, axis=1).astype(np.float64) / ghz / 1e3   # us
+    for j, name in enumerate(PHASES):
+        print(f"  {name:24s} median {np.median(d[:, j]):6.3f} us   p90 {np.percentile(d[:, j], 90):6.3f} us   "
+              f"max {d[:, j].max():6.3f} us")
+    env.close()
+
+
+if __name__ == "__main__":
+    main()
