@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--dt", type=float, default=0.01)
     ap.add_argument("--task", default="hover", choices=["hover", "forward_flight", "heli"])
+    ap.add_argument("--reset-mode", default="template", choices=["template", "retrim"],
+                    help="auto-reset state: mean-wind trim template (default) or per-reset device re-trim (F8)")
     ap.add_argument("--graph-steps", type=int, default=100, help="steps captured per hipGraph")
     ap.add_argument("--gather-obs", action="store_true", help="RCCL all-gather of obs every step")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
@@ -128,7 +130,7 @@ def main():
     dev = torch.device(f"cuda:{torch.cuda.current_device()}")
     N = args.envs
     env = HeliVecEnv(N, task=args.task, dt=args.dt, seed=1234, autoreset=True, env_offset=rank * N,
-                     device=dev)
+                     device=dev, reset_mode=args.reset_mode)
     env.reset()
 
     B = max(1, args.graph_steps)
@@ -215,10 +217,12 @@ def main():
         "dtype": "fp32",
         "data": "synthetic: U(-1,1) Philox actions (HBM-resident bank of %d steps), Philox turbulence" % B,
         "config": {"workload": f"{'HeliHover-v0' if args.task == 'hover' else args.task} x {N} envs/GPU, "
-                               f"Dryden turbulence level 1, dt={args.dt}, auto-reset, "
+                               f"Dryden turbulence level 1, dt={args.dt}, auto-reset"
+                               f"{' (re-trim per reset, F8)' if args.reset_mode == 'retrim' else ''}, "
                                f"{'hipGraph of %d steps' % B if graph is not None else 'eager'}"
                                + (", RCCL obs all-gather every step" if gathered is not None else ""),
-                   "envs_per_gpu": N, "dt": args.dt, "task": args.task, "parallelism": f"env-shard x{world}"},
+                   "envs_per_gpu": N, "dt": args.dt, "task": args.task, "reset_mode": args.reset_mode,
+                   "parallelism": f"env-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": f"step_kernel<{args.task.upper()}>", "kernel_avg_us": kern_s * 1e6,

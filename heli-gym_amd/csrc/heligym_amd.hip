@@ -22,6 +22,7 @@
 
 #include "../../include/heligym_amd.h"
 #include "physics.h"
+#include "trim.h"
 
 using hg::Params;
 using hg::Template;
@@ -88,6 +89,9 @@ struct StepArgs {
     int32_t* reset_count;
     int32_t* reset_index;
     float* final_obs;
+    float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
+    int32_t* retrim_list;    // ... compacted ids of the envs to re-trim
+    int32_t* retrim_count;   // ... their number (zeroed before the launch)
     int64_t n;
     uint64_t seed;
     int64_t env_offset;
@@ -261,6 +265,12 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
 #pragma unroll
     for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
     TSTAMP(8, "v"(hs[8]), "v"(hs[11]), "v"(obs[16]));
+    if (P.reset_retrim && active) {   // F8: a reset this step is trimmed against this wind
+        float* wb = a.retrim_wind + 3 * blk0;
+        st_lane<false>(wb + 0, 3 * (uint32_t)tid, W[0]);
+        st_lane<false>(wb + 1, 3 * (uint32_t)tid, W[1]);
+        st_lane<false>(wb + 2, 3 * (uint32_t)tid, W[2]);
+    }
     // reset template (heli[18] | carry[4] | obs[17]) one float per lane, fetched now so that its
     // latency hides behind the reward / flag work and a reset costs no round trip at the end
     const float tpl = lane < kTplFloats ? reinterpret_cast<const float*>(Tp)[lane] : 0.f;
@@ -314,6 +324,16 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
                     for (int c = 0; c < 17; ++c) a.final_obs[(int64_t)slot * 17 + c] = obs[c];
                 }
             }
+        }
+    }
+    if (P.reset_retrim) {   // queue the resets for retrim_kernel (which overwrites the template)
+        const unsigned long long mask = __ballot(do_reset);
+        if (mask) {
+            const int leader = __ffsll((long long)mask) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(a.retrim_count, __popcll(mask));
+            base = __shfl(base, leader);
+            if (do_reset) a.retrim_list[base + __popcll(mask & ((1ull << lane) - 1ull))] = (int32_t)i;
         }
     }
     if (do_reset) {
@@ -374,6 +394,218 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     TSTAMP(12, "v"(tid));
     if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][14] = __builtin_amdgcn_s_memrealtime();
 #endif
+}
+
+// ------------------------------------------------------------------------------ device re-trim
+// HelicopterDynamics.trim (helicopter_dynamics.py:491-555) for many winds at once: the reset path of
+// reset_mode RETRIM (F8) and hg_trim_batch.  One wave per trim, fp64 throughout, every lane holding
+// the same Newton iterate:
+//   * lanes 0..15 / 16..31 evaluate the +eps / -eps Jacobian columns in parallel;
+//   * lane j <= 16 then holds column j of [J | r] in registers and the Gauss-Jordan elimination
+//     (hg::solve16, same operation order) runs with the pivot column broadcast by readlane;
+//   * lanes 0..9 evaluate the ten step-halving trials at once; the first one that lowers the
+//     residual is the trial the reference's sequential search accepts.
+struct RetrimArgs {
+    const Params<double>* P;
+    const hg::TrimSetup* T;
+    const int32_t* count;   // env mode: device job count; batch mode: NULL (count = njobs)
+    int64_t njobs;
+    const int32_t* list;    // env mode: env id of each job
+    const float* wind;      // [N,3] by env id (env mode) or [count,3] by job (batch mode)
+    float* state;           // env mode: SoA state (heli 18 and carry 4 rewritten)
+    float* obs;             // env mode: [N,17] reset observation rows, or NULL
+    int64_t n;
+    float* out_state;       // batch mode outputs (rows by job), each may be NULL
+    float* out_action;
+    float* out_obs;
+    int32_t* out_status;
+    int32_t* fail_count;    // env mode: trims that failed (env keeps the template reset)
+};
+
+__device__ __forceinline__ double read_lane(double v, int lane) {
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = __shfl((int)(uint32_t)u, src);
+    const uint32_t hi = __shfl((int)(uint32_t)(u >> 32), src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, int64_t env, const double x[16],
+                                             const double s[18], const double ob[17]) {
+    if (a.list) {
+        for (int c = 0; c < 18; ++c) a.state[(int64_t)c * a.n + env] = (float)s[c];
+        const int co[4] = {4, 5, 6, 16};
+        for (int c = 0; c < 4; ++c) a.state[(int64_t)(23 + c) * a.n + env] = (float)ob[co[c]];
+        if (a.obs)
+            for (int c = 0; c < 17; ++c) a.obs[env * 17 + c] = (float)ob[c];
+    } else {
+        if (a.out_state)
+            for (int c = 0; c < 18; ++c) a.out_state[job * 18 + c] = (float)s[c];
+        if (a.out_action)
+            for (int c = 0; c < 4; ++c) a.out_action[job * 4 + c] = (float)x[12 + c];
+        if (a.out_obs)
+            for (int c = 0; c < 17; ++c) a.out_obs[job * 17 + c] = (float)ob[c];
+    }
+    if (a.out_status) a.out_status[job] = HG_OK;
+}
+
+// Lane roles per evaluation round: lanes 0..31 the Jacobian columns at the point the next Newton
+// step will start from, lanes 32..41 the ten step-halving trials of the current step (trial 0,
+// the full step, is that point whenever the search accepts it, which it usually does), lane 32
+// alone the residual at x0 in the first round.  A round is one trim_fcn latency; a trim of three
+// Newton steps takes four rounds.
+__global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
+    const int l = threadIdx.x;
+    const Params<double>& P = *a.P;
+    const hg::TrimSetup& T = *a.T;
+    const double eps = hg::kTrimEps;
+    const int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
+    for (int64_t job = blockIdx.x; job < jobs; job += gridDim.x) {   // uniform per wave
+        const int64_t env = a.list ? (int64_t)a.list[job] : job;
+        const float* wr = a.wind + 3 * (a.list ? env : job);
+        const double W[3] = {(double)wr[0], (double)wr[1], (double)wr[2]};
+        double x[16], y[16], dir[16];
+        for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; }
+        double tol = 0;
+        int it = 0;
+        bool ok = true, done = false, first = true, have_jac = false;
+        while (!done) {
+            // ---- one evaluation round
+            const int c = l & 15;
+            const int j = l - 32;   // line-search trial of this lane (0..9), first round: base point
+            double xe[16];
+            if (l < 32) {   // Jacobian columns at x - dir (= x in the first round)
+                for (int k = 0; k < 16; ++k) {
+                    const double xs = first ? x[k] : x[k] - 1.0 * dir[k];
+                    xe[k] = k == c ? (l < 16 ? xs + eps : xs - eps) : xs;
+                }
+            } else {
+                const double step = (j >= 0 && j < hg::kTrimLineSearch) ? ldexp(1.0, -j) : 0.0;
+                for (int k = 0; k < 16; ++k) xe[k] = first ? x[k] : x[k] - step * dir[k];
+            }
+            double ye[16], se[18], de[18], oe[17];
+            hg::trim_fcn(P, T.base, xe, W, T.hc, ye, se, de, oe);
+            const double te = hg::trim_residual(ye, T.yt);
+            // ---- accept a trial (or take the base point)
+            int src = 32;   // lane whose evaluation is the new iterate
+            if (first) {
+                first = false;
+                have_jac = true;
+            } else {
+                int js = hg::kTrimLineSearch;
+                for (int jj = hg::kTrimLineSearch - 1; jj >= 0; --jj)
+                    if (read_lane(te, 32 + jj) < tol) js = jj;
+                if (js >= hg::kTrimLineSearch - 1) {   // helicopter_dynamics.py:540: keep x
+                    done = true;
+                    src = -1;
+                } else {
+                    const double step = ldexp(1.0, -js);
+                    for (int k = 0; k < 16; ++k) x[k] = x[k] - step * dir[k];
+                    src = 32 + js;
+                    have_jac = js == 0;   // the Jacobian lanes evaluated around trial 0
+                    if (++it > hg::kTrimMaxIter) { ok = false; done = true; src = -1; }
+                }
+            }
+            if (src >= 0) {
+                for (int k = 0; k < 16; ++k) y[k] = read_lane(ye[k], src);
+                tol = read_lane(te, src);
+                if (!(tol > eps)) {   // converged: the accepting lane holds the final evaluation
+                    done = true;
+                    if (l == src) retrim_write(a, job, env, x, se, oe);
+                    break;
+                }
+            }
+            if (done) break;
+            if (!have_jac) {   // the search accepted a shorter step: Jacobian at the new x
+                if (l < 32) {
+                    for (int k = 0; k < 16; ++k) xe[k] = k == c ? (l < 16 ? x[k] + eps : x[k] - eps) : x[k];
+                    hg::trim_fcn(P, T.base, xe, W, T.hc, ye, nullptr, nullptr, nullptr);
+                }
+            }
+            // ---- Newton direction: Gauss-Jordan (hg::solve16), lane j <= 16 owns column j of [J | r]
+            double col[16];
+            for (int k = 0; k < 16; ++k) {
+                const double ym = shfl_d(ye[k], (l + 16) & 63);
+                col[k] = l < 16 ? (ye[k] - ym) / (2 * eps) : y[k] - T.yt[k];
+            }
+#pragma unroll
+            for (int cc = 0; cc < 16; ++cc) {
+                double bc[16];   // column cc, broadcast to every lane
+#pragma unroll
+                for (int k = 0; k < 16; ++k) bc[k] = read_lane(col[k], cc);
+                int p = cc;
+#pragma unroll
+                for (int i = cc + 1; i < 16; ++i)
+                    if (fabs(bc[i]) > fabs(bc[p])) p = i;
+                p = __builtin_amdgcn_readfirstlane(p);
+                double mp = bc[cc];
+#pragma unroll
+                for (int i = cc + 1; i < 16; ++i)
+                    if (i == p) mp = bc[i];
+                if (mp == 0.0 || !isfinite(mp)) { ok = false; break; }
+                if (p != cc) {
+#pragma unroll
+                    for (int i = cc + 1; i < 16; ++i)
+                        if (i == p) {
+                            double t = col[cc]; col[cc] = col[i]; col[i] = t;
+                            t = bc[cc]; bc[cc] = bc[i]; bc[i] = t;
+                        }
+                }
+                const double piv = bc[cc];
+                if (l >= cc) col[cc] /= piv;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    if (i == cc) continue;
+                    const double f = bc[i];
+                    if (l >= cc && f != 0.0) col[i] -= f * col[cc];
+                }
+            }
+            if (!ok) break;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) dir[k] = read_lane(col[k], 16);
+        }
+        if (ok && done && l == 0) {
+            // the search stopped without converging (:540): final evaluation at the kept x
+            bool written = !(tol > eps);
+            if (!written) {
+                double yy[16], s[18], d[18], ob[17];
+                hg::trim_fcn(P, T.base, x, W, T.hc, yy, s, d, ob);
+                retrim_write(a, job, env, x, s, ob);
+            }
+        }
+        if (!ok && l == 0) {
+            if (a.fail_count) atomicAdd(a.fail_count, 1);
+            if (a.out_status) a.out_status[job] = HG_E_TRIM;
+        }
+    }
+}
+
+// reset_mode RETRIM bookkeeping: the wind each env's next reset is trimmed against (the mean wind
+// until the env has stepped, helicopter.py:55), and the compacted list of masked envs of hg_reset.
+__global__ __launch_bounds__(kBlock) void fill_wind_kernel(float* wind, int64_t n, float w0, float w1, float w2) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    wind[3 * i + 0] = w0;
+    wind[3 * i + 1] = w1;
+    wind[3 * i + 2] = w2;
+}
+
+__global__ __launch_bounds__(kBlock) void mask_list_kernel(const uint8_t* mask, int64_t n, int32_t* list,
+                                                           int32_t* count) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool take = i < n && (!mask || mask[i]);
+    const unsigned long long m = __ballot(take);
+    if (!m) return;
+    const int lane = threadIdx.x & 63, leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(count, __popcll(m));
+    base = __shfl(base, leader);
+    if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
 }
 
 // Heli.reset for masked envs (helicopter.py:208-217)
@@ -586,91 +818,40 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
     P.time_up_steps = first_step_above(dt, c.max_time, true);
     P.success_steps = first_step_above(dt, c.max_time / 4, false);
     P.autoreset = c.autoreset ? 1 : 0;
+    P.reset_retrim = (c.autoreset && c.reset_mode == HG_RESET_RETRIM) ? 1 : 0;
     return P;
 }
 
-// helicopter_dynamics.py:557-576 (__trim_fcn): normalised derivatives at the trial point x.  The
-// reference writes the trial point into its float32 state array, so it is rounded to float here.
-void trim_fcn(const Params<double>& P, const double base[18], const double x[16], const double W[3],
-              const hg::Ground<double>& h_c, double y[16], double* s_out, double* d_out, double* obs) {
-    double s[18];
-    memcpy(s, base, sizeof(s));
-    s[0] = (float)(x[0] * P.mr_VTIP);
-    s[1] = (float)(x[1] * P.tr_VTIP);
-    s[4] = (float)x[2];
-    s[5] = (float)x[3];
-    for (int i = 0; i < 3; ++i) {
-        s[6 + i] = (float)(x[4 + i] * P.mr_VTIP);
-        s[9 + i] = (float)(x[7 + i] * P.mr_OMEGA);
-    }
-    s[12] = (float)x[10];
-    s[13] = (float)x[11];
-    const hg::Controls<double> u = hg::controls(P, x[12], x[13], x[14], x[15]);
-    double d[18], ob[17];
-    hg::dynamics<true>(P, s, u, W, h_c, hg::attitude(s + 12), d, ob);
-    y[0] = d[0] / P.mr_VTIP;
-    y[1] = d[1] / P.tr_VTIP;
-    y[2] = d[4];
-    y[3] = d[5];
-    for (int i = 0; i < 3; ++i) {
-        y[4 + i] = d[6 + i] / P.mr_VTIP;
-        y[7 + i] = d[9 + i] / P.mr_OMEGA;
-        y[10 + i] = d[12 + i];
-        y[13 + i] = d[15 + i] / P.mr_R;
-    }
-    if (s_out) memcpy(s_out, s, sizeof(s));
-    if (d_out) memcpy(d_out, d, sizeof(d));
-    if (obs) memcpy(obs, ob, sizeof(ob));
+// Trim setup for a condition (helicopter_dynamics.py:498-516): the fixed state entries, targets
+// and initial guess; the ground under the trim position comes from the host copy of the terrain.
+hg::TrimSetup trim_setup(const Params<double>& P, const float2* hmap, const hg_trim_cond& tc) {
+    hg::TrimSetup t;
+    memset(&t, 0, sizeof(t));
+    t.base[14] = (float)tc.yaw;
+    t.base[2] = (float)tc.psi_mr;
+    t.base[3] = (float)tc.psi_tr;
+    t.base[15] = (float)tc.xy[0];
+    t.base[16] = (float)tc.xy[1];
+    t.hc = hg::ground_height(P, hmap, t.base[15], t.base[16]);
+    t.base[17] = (float)(-(t.hc.h() + P.wl_cg_ft) - tc.gr_alt);
+    t.yt[12] = (float)tc.yaw_rate;
+    for (int i = 0; i < 3; ++i) t.yt[13 + i] = (float)tc.ned_vel[i] / (float)P.mr_R;
+    const double x0[16] = {0.05f, 0.05f, 0, 0, 0, 0, 0, 0, 0, (float)tc.yaw_rate, -0.01f, 0.01f, 0, 0, 0, 0};
+    for (int i = 0; i < 16; ++i) t.x0[i] = x0[i];
+    for (int i = 0; i < 3; ++i) t.x0[4 + i] = (float)tc.ned_vel[i] / (float)P.mr_VTIP;
+    return t;
 }
 
-// np.linalg.inv(dydx) @ r via Gauss-Jordan with partial pivoting
-bool solve16(double A[16][16], const double r[16], double v[16]) {
-    double M[16][17];
-    for (int i = 0; i < 16; ++i) {
-        for (int j = 0; j < 16; ++j) M[i][j] = A[i][j];
-        M[i][16] = r[i];
-    }
-    for (int c = 0; c < 16; ++c) {
-        int p = c;
-        for (int i = c + 1; i < 16; ++i)
-            if (fabs(M[i][c]) > fabs(M[p][c])) p = i;
-        if (M[p][c] == 0.0 || !std::isfinite(M[p][c])) return false;
-        if (p != c)
-            for (int j = 0; j < 17; ++j) std::swap(M[c][j], M[p][j]);
-        const double piv = M[c][c];
-        for (int j = c; j < 17; ++j) M[c][j] /= piv;
-        for (int i = 0; i < 16; ++i) {
-            if (i == c) continue;
-            const double f = M[i][c];
-            if (f != 0.0)
-                for (int j = c; j < 17; ++j) M[i][j] -= f * M[c][j];
-        }
-    }
-    for (int i = 0; i < 16; ++i) v[i] = M[i][16];
-    return true;
-}
-
-// HelicopterDynamics.trim (helicopter_dynamics.py:491-555), fp64 Newton with a central-difference
-// Jacobian and step halving, identical iteration logic to the reference.
+// HelicopterDynamics.trim (helicopter_dynamics.py:491-555), serial: fp64 Newton with a central-
+// difference Jacobian and step halving, the reference's iteration logic.
 int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond& tc, const double W[3],
                 hg_trim_result* out) {
-    double base[18] = {0};
-    base[14] = (float)tc.yaw;
-    base[2] = (float)tc.psi_mr;
-    base[3] = (float)tc.psi_tr;
-    base[15] = (float)tc.xy[0];
-    base[16] = (float)tc.xy[1];
-    const hg::Ground<double> h_c = hg::ground_height(P, hmap, base[15], base[16]);
-    base[17] = (float)(-(h_c.h() + P.wl_cg_ft) - tc.gr_alt);
-    double yt[16] = {0};
-    yt[12] = (float)tc.yaw_rate;
-    for (int i = 0; i < 3; ++i) yt[13 + i] = (float)tc.ned_vel[i] / (float)P.mr_R;
-    double x[16] = {0.05f, 0.05f, 0, 0, 0, 0, 0, 0, 0, (float)tc.yaw_rate, -0.01f, 0.01f, 0, 0, 0, 0};
-    for (int i = 0; i < 3; ++i) x[4 + i] = (float)tc.ned_vel[i] / (float)P.mr_VTIP;
-    const double eps = 1e-4;
-    double y[16], tol = 0;
-    trim_fcn(P, base, x, W, h_c, y, nullptr, nullptr, nullptr);
-    for (int i = 0; i < 16; ++i) tol += (y[i] - yt[i]) * (y[i] - yt[i]);
+    const hg::TrimSetup T = trim_setup(P, hmap, tc);
+    const double eps = hg::kTrimEps;
+    double x[16], y[16];
+    memcpy(x, T.x0, sizeof(x));
+    hg::trim_fcn(P, T.base, x, W, T.hc, y, nullptr, nullptr, nullptr);
+    double tol = hg::trim_residual(y, T.yt);
     int it = 0;
     while (tol > eps) {
         double J[16][16], yp[16], ym[16], xp[16], xm[16], r[16], dir[16];
@@ -679,30 +860,28 @@ int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond&
             memcpy(xm, x, sizeof(x));
             xp[i] += eps;
             xm[i] -= eps;
-            trim_fcn(P, base, xp, W, h_c, yp, nullptr, nullptr, nullptr);
-            trim_fcn(P, base, xm, W, h_c, ym, nullptr, nullptr, nullptr);
+            hg::trim_fcn(P, T.base, xp, W, T.hc, yp, nullptr, nullptr, nullptr);
+            hg::trim_fcn(P, T.base, xm, W, T.hc, ym, nullptr, nullptr, nullptr);
             for (int k = 0; k < 16; ++k) J[k][i] = (yp[k] - ym[k]) / (2 * eps);
         }
-        for (int k = 0; k < 16; ++k) r[k] = y[k] - yt[k];
-        if (!solve16(J, r, dir)) return fail(HG_E_TRIM, "trim: singular Jacobian");
+        for (int k = 0; k < 16; ++k) r[k] = y[k] - T.yt[k];
+        if (!hg::solve16(J, r, dir)) return fail(HG_E_TRIM, "trim: singular Jacobian");
         double step = 1.0, xn[16], yn[16], tn = 0;
         int j;
-        for (j = 0; j < 10; ++j) {
+        for (j = 0; j < hg::kTrimLineSearch; ++j) {
             for (int k = 0; k < 16; ++k) xn[k] = x[k] - step * dir[k];
-            trim_fcn(P, base, xn, W, h_c, yn, nullptr, nullptr, nullptr);
-            tn = 0;
-            for (int k = 0; k < 16; ++k) tn += (yn[k] - yt[k]) * (yn[k] - yt[k]);
+            hg::trim_fcn(P, T.base, xn, W, T.hc, yn, nullptr, nullptr, nullptr);
+            tn = hg::trim_residual(yn, T.yt);
             step *= 0.5;
             if (tn < tol) break;
         }
-        if (j >= 9) break;   // :540
+        if (j >= hg::kTrimLineSearch - 1) break;   // :540
         memcpy(x, xn, sizeof(x));
         memcpy(y, yn, sizeof(y));
         tol = tn;
-        if (++it > 200)   // the reference gives up after 5 s (:543-544)
-            return fail(HG_E_TRIM, "Trim failed, please try a better trim condition!");
+        if (++it > hg::kTrimMaxIter) return fail(HG_E_TRIM, "Trim failed, please try a better trim condition!");
     }
-    trim_fcn(P, base, x, W, h_c, y, out->state, out->state_dots, out->obs);
+    hg::trim_fcn(P, T.base, x, W, T.hc, y, out->state, out->state_dots, out->obs);
     for (int i = 0; i < 4; ++i) out->action[i] = x[12 + i];
     out->residual = tol;
     out->iterations = it;
@@ -717,6 +896,8 @@ int32_t check_config(const hg_config* c, int32_t rows, int32_t cols) {
     if (!(c->max_time > 0)) return fail(HG_E_INVALID, "max_time must be > 0");
     if (c->task < HG_TASK_HELI || c->task > HG_TASK_FORWARD_FLIGHT) return fail(HG_E_INVALID, "bad task");
     if (c->af.env_TURB_LVL < 0 || c->af.env_TURB_LVL > 7) return fail(HG_E_INVALID, "TURB_LVL must be 0..7");
+    if (c->reset_mode != HG_RESET_TEMPLATE && c->reset_mode != HG_RESET_RETRIM)
+        return fail(HG_E_INVALID, "reset_mode must be HG_RESET_TEMPLATE or HG_RESET_RETRIM");
     if (rows < 2 || cols < 2 || rows != cols)
         return fail(HG_E_INVALID, "terrain must be a square map of at least 2x2 samples");
     return HG_OK;
@@ -741,12 +922,19 @@ struct hg_env {
     Params<float>* params_dev = nullptr;
     hg_trim_result trim;
     int64_t resident_envs = 0;   // one wave per SIMD on this device: 64 lanes x 4 SIMDs x CUs
+    hg::TrimSetup setup;                    // trim condition -> Newton setup (host copy)
+    hg::TrimSetup* setup_dev = nullptr;     // ... and device copy (re-trim kernel)
+    Params<double>* pd_dev = nullptr;       // fp64 model constants for the re-trim kernel
+    float* retrim_wind = nullptr;           // reset_mode RETRIM work buffers
+    int32_t* retrim_list = nullptr;
+    int32_t* retrim_count = nullptr;        // [0] jobs of the current step, [1] failures so far
 };
 
 // Upload the fp32 model constants the step kernel reads (after create and every setter).
 static int32_t upload_params(hg_env* e) {
     if (!e->params_dev) return HG_OK;
     hipError_t err = hipMemcpy(e->params_dev, &e->Pf, sizeof(e->Pf), hipMemcpyHostToDevice);
+    if (err == hipSuccess && e->pd_dev) err = hipMemcpy(e->pd_dev, &e->Pd, sizeof(e->Pd), hipMemcpyHostToDevice);
     if (err != hipSuccess) return fail(HG_E_HIP, std::string("params upload: ") + hipGetErrorString(err));
     return HG_OK;
 }
@@ -764,14 +952,21 @@ static int32_t build_template(hg_env* e) {
     e->tmpl.carry[1] = (float)r.obs[5];
     e->tmpl.carry[2] = (float)r.obs[6];
     e->tmpl.carry[3] = (float)r.obs[16];
-    if (e->tmpl_dev) {   // device copy read by the step kernel's auto-reset (stream-ordered after prior work)
+    e->setup = trim_setup(e->Pd, e->hmap_host.data(), e->cfg.trim);
+    if (e->tmpl_dev) {   // device copies read by the step / re-trim kernels (after prior work)
         hipError_t err = hipMemcpy(e->tmpl_dev, &e->tmpl, sizeof(e->tmpl), hipMemcpyHostToDevice);
+        if (err == hipSuccess && e->setup_dev)
+            err = hipMemcpy(e->setup_dev, &e->setup, sizeof(e->setup), hipMemcpyHostToDevice);
         if (err != hipSuccess) return fail(HG_E_HIP, std::string("template upload: ") + hipGetErrorString(err));
     }
     return HG_OK;
 }
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+// re-trim launches: one job per 64-lane block, at most 1024 blocks (jobs beyond loop)
+static inline unsigned retrim_grid(int64_t jobs) {
+    return (unsigned)(jobs < 1 ? 1 : (jobs > 1024 ? 1024 : jobs));
+}
 
 #if HG_PARAMS_PTR
 #define PARAM_ARG(e) ((const Params<float>*)(e)->params_dev)
@@ -863,6 +1058,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if (rc != HG_OK) { delete e; return rc; }
     auto cleanup = [&](hipError_t err, const char* what) {
         dfree(e->hmap); dfree(e->state); dfree(e->counters); dfree(e->tmpl_dev); dfree(e->params_dev);
+        dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_count);
         delete e;
         return fail(HG_E_HIP, std::string(what) + ": " + hipGetErrorString(err));
     };
@@ -883,6 +1079,23 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if ((err = hipMalloc(&e->tmpl_dev, sizeof(Template<float>))) != hipSuccess) return cleanup(err, "hipMalloc template");
     if ((err = hipMemcpy(e->tmpl_dev, &e->tmpl, sizeof(e->tmpl), hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy template");
+    if ((err = hipMalloc(&e->setup_dev, sizeof(hg::TrimSetup))) != hipSuccess) return cleanup(err, "hipMalloc setup");
+    if ((err = hipMemcpy(e->setup_dev, &e->setup, sizeof(e->setup), hipMemcpyHostToDevice)) != hipSuccess)
+        return cleanup(err, "hipMemcpy setup");
+    if ((err = hipMalloc(&e->pd_dev, sizeof(Params<double>))) != hipSuccess) return cleanup(err, "hipMalloc params64");
+    if ((err = hipMemcpy(e->pd_dev, &e->Pd, sizeof(e->Pd), hipMemcpyHostToDevice)) != hipSuccess)
+        return cleanup(err, "hipMemcpy params64");
+    if ((err = hipMalloc(&e->retrim_count, 2 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim");
+    if ((err = hipMemset(e->retrim_count, 0, 2 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim");
+    if (cfg->reset_mode == HG_RESET_RETRIM) {
+        if ((err = hipMalloc(&e->retrim_wind, sizeof(float) * 3 * num_envs)) != hipSuccess)
+            return cleanup(err, "hipMalloc retrim wind");
+        if ((err = hipMalloc(&e->retrim_list, sizeof(int32_t) * num_envs)) != hipSuccess)
+            return cleanup(err, "hipMalloc retrim list");
+        hipLaunchKernelGGL(fill_wind_kernel, dim3(grid_for(num_envs)), dim3(kBlock), 0, 0, e->retrim_wind, num_envs,
+                           (float)e->Pd.wm[0], (float)e->Pd.wm[1], (float)e->Pd.wm[2]);
+        if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "fill_wind_kernel");
+    }
     hipLaunchKernelGGL(init_kernel, dim3(grid_for(num_envs)), dim3(kBlock), 0, 0, e->tmpl, e->state, e->counters, num_envs);
     if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "init_kernel");
     if ((err = hipDeviceSynchronize()) != hipSuccess) return cleanup(err, "init sync");
@@ -897,6 +1110,11 @@ void hg_destroy(hg_env* e) {
     dfree(e->counters);
     dfree(e->tmpl_dev);
     dfree(e->params_dev);
+    dfree(e->setup_dev);
+    dfree(e->pd_dev);
+    dfree(e->retrim_wind);
+    dfree(e->retrim_list);
+    dfree(e->retrim_count);
     delete e;
 }
 
@@ -935,9 +1153,28 @@ int32_t hg_get_template(const hg_env* e, hg_trim_result* out) {
 
 int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
-    hipLaunchKernelGGL(reset_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->tmpl,
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(reset_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->tmpl,
                        e->state, e->counters, mask, obs, e->n);
     HIP_TRY(hipGetLastError());
+    if (e->cfg.reset_mode == HG_RESET_RETRIM) {   // trim each masked env against its last wind (F8)
+        HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
+        hipLaunchKernelGGL(mask_list_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, mask, e->n, e->retrim_list,
+                           e->retrim_count);
+        RetrimArgs r;
+        memset(&r, 0, sizeof(r));
+        r.P = e->pd_dev;
+        r.T = e->setup_dev;
+        r.count = e->retrim_count;
+        r.list = e->retrim_list;
+        r.wind = e->retrim_wind;
+        r.state = e->state;
+        r.obs = obs;
+        r.n = e->n;
+        r.fail_count = e->retrim_count + 1;
+        hipLaunchKernelGGL(retrim_kernel, dim3(retrim_grid(e->n)), dim3(64), 0, s, r);
+        HIP_TRY(hipGetLastError());
+    }
     return HG_OK;
 }
 
@@ -953,6 +1190,8 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
         return fail(HG_E_INVALID, "reset_index/final_obs need reset_count");
     hipStream_t s = (hipStream_t)stream;
     if (reset_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
+    const bool retrim = e->Pf.reset_retrim != 0;
+    if (retrim) HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
     StepArgs a;
     a.state = e->state;
     a.counters = e->counters;
@@ -967,6 +1206,9 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     a.reset_count = reset_count;
     a.reset_index = reset_index;
     a.final_obs = final_obs;
+    a.retrim_wind = e->retrim_wind;
+    a.retrim_list = e->retrim_list;
+    a.retrim_count = e->retrim_count;
     a.n = e->n;
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;
@@ -987,8 +1229,51 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
         default: HG_LAUNCH_STEP(HG_TASK_HELI); break;
     }
 #undef HG_LAUNCH_STEP_NT
+    HIP_TRY(hipGetLastError());
+    if (retrim) {   // re-trim this step's resets against their last wind (overwrites the template)
+        RetrimArgs r;
+        memset(&r, 0, sizeof(r));
+        r.P = e->pd_dev;
+        r.T = e->setup_dev;
+        r.count = e->retrim_count;
+        r.list = e->retrim_list;
+        r.wind = e->retrim_wind;
+        r.state = e->state;
+        r.obs = obs;
+        r.n = e->n;
+        r.fail_count = e->retrim_count + 1;
+        hipLaunchKernelGGL(retrim_kernel, dim3(retrim_grid(e->n)), dim3(64), 0, s, r);
+    }
 #undef HG_LAUNCH_STEP
     HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_trim_batch(hg_env* e, const float* wind, int64_t count, float* state, float* action, float* obs,
+                      int32_t* status, void* stream) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    if (count < 0 || (count > 0 && !wind)) return fail(HG_E_INVALID, "bad wind / count");
+    if (count == 0) return HG_OK;
+    RetrimArgs r;
+    memset(&r, 0, sizeof(r));
+    r.P = e->pd_dev;
+    r.T = e->setup_dev;
+    r.njobs = count;
+    r.wind = wind;
+    r.out_state = state;
+    r.out_action = action;
+    r.out_obs = obs;
+    r.out_status = status;
+    hipLaunchKernelGGL(retrim_kernel, dim3(retrim_grid(count)), dim3(64), 0, (hipStream_t)stream, r);
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_retrim_failures(hg_env* e, int64_t* count) {
+    if (!e || !count) return fail(HG_E_INVALID, "bad env or count");
+    int32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, e->retrim_count + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
+    *count = v;
     return HG_OK;
 }
 

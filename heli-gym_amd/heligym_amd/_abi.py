@@ -21,6 +21,9 @@ HG_COUNTER_COLS = 3
 HG_OK = 0
 HG_TASK_HELI, HG_TASK_HOVER, HG_TASK_FORWARD_FLIGHT = 0, 1, 2
 HG_INFO_FAILED, HG_INFO_SUCCESSED, HG_INFO_TIME_UP, HG_INFO_SUCCESS_STEP = 1, 2, 4, 8
+HG_RESET_TEMPLATE, HG_RESET_RETRIM = 0, 1
+RESET_MODES = {"template": HG_RESET_TEMPLATE, "retrim": HG_RESET_RETRIM}
+HG_ABI_VERSION = 2
 
 AIRFRAME_FIELDS = (
     ["env_R", "env_T0", "env_LAPSE", "env_RO_SEA", "env_GRAV", "env_MAX_GR_ALT", "env_NS_MAX",
@@ -59,7 +62,8 @@ class hg_config(ctypes.Structure):
     _fields_ = [("af", hg_airframe), ("trim", hg_trim_cond), ("target", hg_target),
                 ("dt", ctypes.c_double), ("max_time", ctypes.c_double),
                 ("task", ctypes.c_int32), ("autoreset", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("env_offset", ctypes.c_int64)]
+                ("seed", ctypes.c_uint64), ("env_offset", ctypes.c_int64),
+                ("reset_mode", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class hg_trim_result(ctypes.Structure):
@@ -91,6 +95,8 @@ _SIGS = {
     "hg_set_state": (ctypes.c_int32, [_P, _P, _P, _P]),
     "hg_random_actions": (ctypes.c_int32, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,
                                            ctypes.c_float, _P]),
+    "hg_trim_batch": (ctypes.c_int32, [_P, _P, ctypes.c_int64, _P, _P, _P, _P, _P]),
+    "hg_retrim_failures": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 
@@ -121,7 +127,7 @@ def load_library(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.hg_abi_version() != 1:
+    if lib.hg_abi_version() != HG_ABI_VERSION:
         raise HeliGymError("ABI version mismatch")
     if path is None:
         _lib = lib

@@ -73,7 +73,8 @@ def fill_target(tg, target):
 
 
 def make_config(task="hover", dt=DT, heli_name="aw109", max_time=None, target=None,
-                trim_cond=None, autoreset=True, seed=0, env_offset=0, turbulence_level=None):
+                trim_cond=None, autoreset=True, seed=0, env_offset=0, turbulence_level=None,
+                reset_mode="template"):
     doc = load_airframe(heli_name)
     cfg = _abi.hg_config()
     af = doc["airframe"]
@@ -96,4 +97,7 @@ def make_config(task="hover", dt=DT, heli_name="aw109", max_time=None, target=No
     cfg.autoreset = 1 if autoreset else 0
     cfg.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     cfg.env_offset = int(env_offset)
+    if reset_mode not in _abi.RESET_MODES:
+        raise ValueError(f"unknown reset_mode {reset_mode!r}; one of {sorted(_abi.RESET_MODES)}")
+    cfg.reset_mode = _abi.RESET_MODES[reset_mode]
     return cfg, doc

@@ -62,7 +62,7 @@ class HeliVecEnv:
 
     def __init__(self, num_envs, task="hover", dt=config.DT, heli_name="aw109", seed=0, device=None,
                  autoreset=True, env_offset=0, max_time=None, target=None, trim_cond=None,
-                 turbulence_level=None):
+                 turbulence_level=None, reset_mode="template"):
         import torch
         self.torch = torch
         self.lib = _abi.load_library()
@@ -76,7 +76,8 @@ class HeliVecEnv:
         self.cfg, doc = config.make_config(task=task, dt=dt, heli_name=heli_name, max_time=max_time,
                                            target=target, trim_cond=trim_cond, autoreset=autoreset,
                                            seed=seed, env_offset=env_offset,
-                                           turbulence_level=turbulence_level)
+                                           turbulence_level=turbulence_level, reset_mode=reset_mode)
+        self.reset_mode = reset_mode
         u16 = config.load_terrain(doc)
         self.terrain_ft = config.terrain_ft(u16, self.cfg.af.env_MAX_GR_ALT)
         self._target = dict(config.DEFAULT_TARGETS[task])
@@ -232,6 +233,31 @@ class HeliVecEnv:
             raise ValueError("counters must be [N, 3]")
         self._check(self.lib.hg_set_state(self._h, _ptr(s), _ptr(c), self._stream()))
         self._keep_state = (s, c)
+
+    def trim_batch(self, wind_ned):
+        """Device batched trim (hg_trim_batch) of this env's trim condition against each row of
+        `wind_ned` [K,3] (ft/s NED): the reset the reference computes from its second episode on.
+        Returns dict of float32 device tensors state [K,18], action [K,4], obs [K,17] and int32
+        status [K] (0 or HG_E_TRIM)."""
+        t = self.torch
+        w = t.as_tensor(wind_ned, device=self.device, dtype=t.float32).contiguous()
+        if w.ndim != 2 or w.shape[1] != 3:
+            raise ValueError("wind_ned must be [K, 3]")
+        K = w.shape[0]
+        out = {"state": t.empty((K, _abi.HG_N_HELI), dtype=t.float32, device=self.device),
+               "action": t.empty((K, _abi.HG_N_ACT), dtype=t.float32, device=self.device),
+               "obs": t.empty((K, _abi.HG_N_OBS), dtype=t.float32, device=self.device),
+               "status": t.full((K,), -99, dtype=t.int32, device=self.device)}
+        self._check(self.lib.hg_trim_batch(self._h, _ptr(w), K, _ptr(out["state"]), _ptr(out["action"]),
+                                           _ptr(out["obs"]), _ptr(out["status"]), self._stream()))
+        self._keep_trim = w
+        return out
+
+    def retrim_failures(self):
+        """Auto-resets in reset_mode="retrim" whose trim did not converge (they got the template)."""
+        c = ctypes.c_int64()
+        self._check(self.lib.hg_retrim_failures(self._h, ctypes.byref(c)))
+        return c.value
 
     def random_actions(self, out, seed, step, lo=-1.0, hi=1.0):
         self._check(self.lib.hg_random_actions(self._h, _ptr(out), int(seed), int(step), float(lo),

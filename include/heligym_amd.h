@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 1
+#define HG_ABI_VERSION 2
 
 #define HG_N_OBS 17        /* helicopter_dynamics.py:23-27 */
 #define HG_N_ACT 4         /* helicopter_dynamics.py:28 */
@@ -52,6 +52,14 @@ enum {
 /* Tasks: helicopter.py:242-243 (Heli, reward 0), helicopter_with_tasks.py:5-52 (HeliHover),
  * helicopter_with_tasks.py:54-115 (HeliForwardFlight). */
 enum { HG_TASK_HELI = 0, HG_TASK_HOVER = 1, HG_TASK_FORWARD_FLIGHT = 2 };
+
+/* Reset state of auto-reset envs (hg_config.reset_mode).
+ *   HG_RESET_TEMPLATE: the trim against the mean wind, computed once (the reference's first reset,
+ *                      helicopter.py:55 + helicopter_dynamics.py:66-71), broadcast in-kernel.
+ *   HG_RESET_RETRIM:   every reset re-trimmed on the device against the wind of the env's last step,
+ *                      as the reference does from its second episode on (the heli model keeps the
+ *                      last set_wind, helicopter.py:198 -> helicopter_dynamics.py:66-71,491-555). */
+enum { HG_RESET_TEMPLATE = 0, HG_RESET_RETRIM = 1 };
 
 /* info bit-field written per env by hg_step (helicopter.py:219-224). */
 enum { HG_INFO_FAILED = 1, HG_INFO_SUCCESSED = 2, HG_INFO_TIME_UP = 4, HG_INFO_SUCCESS_STEP = 8 };
@@ -101,6 +109,8 @@ typedef struct hg_config {
     int32_t autoreset;    /* 1: reset finished envs inside hg_step (same-step autoreset) */
     uint64_t seed;        /* Philox key for the turbulence noise (wind_dynamics.py:49-52) */
     int64_t env_offset;   /* global id of local env 0 (sharding: results independent of rank count) */
+    int32_t reset_mode;   /* HG_RESET_* */
+    int32_t reserved;
 } hg_config;
 
 /* Reset template produced by the trim (host values). */
@@ -151,7 +161,9 @@ int32_t hg_get_template(const hg_env* env, hg_trim_result* out);
 /* Reset: replaces Heli.reset (helicopter.py:208-217) -> WindDynamics.reset (wind_dynamics.py:44-47)
  * + HelicopterDynamics.reset (helicopter_dynamics.py:66-71).  Envs with mask_dev[i] != 0 (all
  * envs if mask_dev == NULL) get the trimmed state, zero turbulence state, zero counters; their
- * observation row is written to obs_dev [N,17] (other rows untouched). */
+ * observation row is written to obs_dev [N,17] (other rows untouched).  In HG_RESET_RETRIM mode
+ * each masked env is trimmed against the wind of its last step (the mean wind before its first
+ * step), as the reference's reset trims against the model's last set_wind. */
 int32_t hg_reset(hg_env* env, const uint8_t* mask_dev, float* obs_dev, void* stream);
 
 /* Step: replaces Heli.step (helicopter.py:192-206) with everything it calls — WindDynamics.step
@@ -174,6 +186,21 @@ int32_t hg_step(hg_env* env, const float* actions_dev, float* obs_dev, float* re
                 uint8_t* terminated_dev, uint8_t* truncated_dev, uint8_t* info_dev,
                 const float* eta_dev, int32_t* reset_count_dev, int32_t* reset_index_dev,
                 float* final_obs_dev, void* stream);
+
+/* Batched device trim: HelicopterDynamics.trim (helicopter_dynamics.py:491-576) of the env's trim
+ * condition against `count` winds at once — the reset path of reset_mode HG_RESET_RETRIM, exposed
+ * for direct use.  Same Newton iteration as hg_trim (fp64, trial point rounded to fp32), with the
+ * 32 Jacobian evaluations and the 10 line-search trials of each step evaluated in parallel lanes.
+ *   wind_dev   [count,3] fp32 in (NED, ft/s)
+ *   state_dev  [count,18] fp32 out or NULL, action_dev [count,4] fp32 out or NULL,
+ *   obs_dev    [count,17] fp32 out or NULL, status_dev [count] i32 out or NULL
+ *              (HG_OK, or HG_E_TRIM where the Newton iteration failed; outputs untouched there) */
+int32_t hg_trim_batch(hg_env* env, const float* wind_dev, int64_t count, float* state_dev, float* action_dev,
+                      float* obs_dev, int32_t* status_dev, void* stream);
+
+/* Number of RETRIM-mode auto-resets so far whose trim failed (those envs got the template state).
+ * Synchronises with the device. */
+int32_t hg_retrim_failures(hg_env* env, int64_t* count);
 
 /* State access for parity tests / checkpointing (the reference's StateNumpy,
  * dynamics.py:75-128, exposed as one record per env): state [N,HG_STATE_COLS] fp32,

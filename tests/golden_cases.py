@@ -143,3 +143,19 @@ def reward_bounds(heli, dots, task, n_t=np.sqrt(2 * 18 / 32.2), n_x=36.0, n_v=np
 
 
 CONTACT_GR_ALT = 10.0   # ft: below this ground altitude the landing gear can be in contact
+
+
+def f8_resets():
+    """Second-episode reset fixtures (tests/golden/reset_f8.npz): (dt, trim cond vector, wind, reset
+    state, reset action, reset obs) for the recorded cases and the crash-ended episodes."""
+    d = np.load(os.path.join(GOLDEN, "reset_f8.npz"), allow_pickle=False)
+    rows = [(float(d["case/dt"][i]), d["case/cond"][i], d["case/wind_ned"][i], d["case/state"][i],
+             d["case/action"][i], d["case/obs"][i]) for i in range(len(d["case/dt"]))]
+    rows += [(float(d["episode/dt"][i]), None, d["episode/wind_ned"][i], d["episode/reset_state"][i],
+              d["episode/reset_action"][i], d["episode/reset_obs"][i]) for i in range(len(d["episode/dt"]))]
+    return rows
+
+
+def f8_episodes():
+    d = np.load(os.path.join(GOLDEN, "reset_f8.npz"), allow_pickle=False)
+    return {k.split("/", 1)[1]: d[k] for k in d.files if k.startswith("episode/")}

@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from conftest import ROOT, load_golden, trim_dict
+import golden_cases
 
 from heligym_amd import _abi, config
 
@@ -106,3 +107,31 @@ def test_vector_env_refuses_without_device():
     from heligym_amd import HeliVecEnv
     with pytest.raises(_abi.HeliGymError):
         HeliVecEnv(8)
+
+
+@pytest.mark.parametrize("i", range(11))
+def test_host_trim_f8_resets(lib, terrain_u16, i):
+    """Second-episode resets (F8): the reference trims against the last step's wind; the host trim
+    given that wind reproduces its reset state, action and observation."""
+    dt, cond, wind, state, action, obs = golden_cases.f8_resets()[i]
+    cfg, _ = config.make_config(dt=dt, trim_cond=trim_dict(cond) if cond is not None else None)
+    hm = config.terrain_ft(terrain_u16, cfg.af.env_MAX_GR_ALT)
+    r = _abi.hg_trim_result()
+    _abi.check(lib.hg_trim(ctypes.byref(cfg), hm.ctypes.data, 1024, 1024, (ctypes.c_double * 3)(*wind),
+                           ctypes.byref(r)), lib)
+    for name, ref in (("state", state), ("action", action), ("obs", obs)):
+        got = np.array(getattr(r, name))
+        assert np.all(np.abs(got - ref) <= 1e-4 * (np.abs(ref) + 1)), (name, got - ref)
+
+
+def test_reset_mode_is_validated(lib, terrain_u16):
+    cfg, _ = config.make_config(reset_mode="retrim")
+    assert cfg.reset_mode == _abi.HG_RESET_RETRIM
+    with pytest.raises(ValueError):
+        config.make_config(reset_mode="sometimes")
+    bad = _abi.hg_config.from_buffer_copy(cfg)
+    bad.reset_mode = 7
+    hm = config.terrain_ft(terrain_u16, cfg.af.env_MAX_GR_ALT)
+    h = ctypes.c_void_p()
+    assert lib.hg_create(ctypes.byref(bad), hm.ctypes.data, 1024, 1024, 16, ctypes.byref(h)) == -1
+    assert b"reset_mode" in lib.hg_last_error()

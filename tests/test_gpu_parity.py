@@ -380,3 +380,115 @@ def test_heli_task_reward_is_zero(torch):
         obs, rew, *_ = env.step(act)
         assert float(rew.abs().max()) == 0.0       # helicopter.py:242-243
     env.close()
+
+
+def _group_f8():
+    groups = {}
+    for dt, cond, wind, state, action, obs in gc.f8_resets():
+        key = (dt, None if cond is None else tuple(cond))
+        groups.setdefault(key, []).append((wind, state, action, obs))
+    return groups
+
+
+def test_trim_batch_matches_reference_f8(torch):
+    """hg_trim_batch (device, 32 lanes per trim) reproduces the reference's second-episode resets
+    (F8) from the recorded winds: state / action / observation within the trim contract."""
+    from conftest import trim_dict
+    worst = 0.0
+    for (dt, cond), rows in _group_f8().items():
+        env = make_env(torch, 64, "hover", dt, trim_cond=None if cond is None else trim_dict(np.array(cond)))
+        out = env.trim_batch(np.array([r[0] for r in rows], np.float32))
+        torch.cuda.synchronize()
+        assert np.all(out["status"].cpu().numpy() == 0)
+        for k, name in ((1, "state"), (2, "action"), (3, "obs")):
+            got = out[name].cpu().numpy().astype(np.float64)
+            ref = np.array([r[k] for r in rows])
+            err = np.abs(got - ref) / (np.abs(ref) + 1)
+            worst = max(worst, float(err.max()))
+            assert np.all(err <= TRIM_REL), (dt, cond, name, err.max(axis=0))
+        env.close()
+    print(f"\n[trim_batch vs reference F8] worst |d|/(|x|+1) = {worst:.2e}")
+
+
+def test_trim_batch_matches_host_trim(torch, terrain_u16):
+    """The device Newton (parallel Jacobian / line search) against the host's serial one for 96 winds
+    around the mean wind, including gusty ones."""
+    import ctypes
+    from heligym_amd import _abi, config
+    lib = _abi.load_library()
+    env = make_env(torch, 64, "hover", 0.01)
+    rng = np.random.RandomState(5)
+    winds = (np.array([14.142136, 14.142136, 0.0]) + rng.normal(0, 4.0, size=(96, 3))).astype(np.float32)
+    out = env.trim_batch(winds)
+    torch.cuda.synchronize()
+    status = out["status"].cpu().numpy()
+    hm = config.terrain_ft(terrain_u16, env.cfg.af.env_MAX_GR_ALT)
+    worst = 0.0
+    for j in range(len(winds)):
+        r = _abi.hg_trim_result()
+        rc = lib.hg_trim(ctypes.byref(env.cfg), hm.ctypes.data, 1024, 1024,
+                         (ctypes.c_double * 3)(*winds[j].astype(np.float64)), ctypes.byref(r))
+        assert (rc == 0) == (status[j] == 0), j
+        if rc != 0:
+            continue
+        for name in ("state", "action", "obs"):
+            ref = np.array(getattr(r, name))
+            got = out[name][j].cpu().numpy().astype(np.float64)
+            err = np.abs(got - ref) / (np.abs(ref) + 1)
+            worst = max(worst, float(err.max()))
+            assert np.all(err <= 1e-5), (j, name, err.max())
+    print(f"\n[trim_batch vs host trim] {int((status == 0).sum())}/{len(winds)} converged, "
+          f"worst |d|/(|x|+1) = {worst:.2e}")
+    env.close()
+
+
+def test_retrim_autoreset_matches_reference_episode(torch):
+    """reset_mode="retrim": an env that crashes is reset in the same step to the trim against the
+    wind of that step, as the reference's next reset() computes (F8)."""
+    ep = gc.f8_episodes()
+    N = 70   # ragged: one env per episode at the front, the rest copies
+    for e in range(len(ep["dt"])):
+        dt = float(ep["dt"][e])
+        env = make_env(torch, N, "hover", dt, autoreset=True, reset_mode="retrim")
+        pre = np.concatenate([ep["pre_state"][e], ep["pre_wind"][e], ep["pre_obs"][e][[4, 5, 6, 16]]])
+        env.set_state(np.tile(pre, (N, 1)).astype(np.float32),
+                      np.tile([int(ep["t"][e]), int(ep["succ_before"][e]), 0], (N, 1)).astype(np.int32))
+        act = torch.as_tensor(np.tile(ep["action"][e], (N, 1)).astype(np.float32), device=env.device)
+        eta = torch.as_tensor(np.tile(ep["eta"][e], (N, 1)).astype(np.float32), device=env.device)
+        obs, rew, term, trunc, info = env.step(act, eta=eta)
+        st, ctr = env.get_state()
+        torch.cuda.synchronize()
+        assert bool(term.all()) and bool(info["failed"].all())
+        s = st.cpu().numpy().astype(np.float64)
+        o = obs.cpu().numpy().astype(np.float64)
+        ref_s, ref_o = ep["reset_state"][e], ep["reset_obs"][e]
+        err_s = np.abs(s[:, :18] - ref_s) / (np.abs(ref_s) + 1)
+        err_o = np.abs(o - ref_o) / (np.abs(ref_o) + 1)
+        print(f"\n[retrim episode {e}] worst state {err_s.max():.2e} obs {err_o.max():.2e}")
+        assert np.all(err_s <= TRIM_REL) and np.all(err_o <= TRIM_REL)
+        np.testing.assert_array_equal(s[:, 18:23], 0.0)
+        np.testing.assert_allclose(s[:, 23:27], o[:, [4, 5, 6, 16]])
+        np.testing.assert_array_equal(ctr.cpu().numpy()[:, :2], 0)
+        # an explicit reset() right after trims against the same last wind (F8): same state again
+        obs2, _ = env.reset()
+        st2, _ = env.get_state()
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(st2.cpu().numpy()[:, :18], s[:, :18], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(obs2.cpu().numpy(), o, rtol=1e-6, atol=1e-6)
+        assert env.retrim_failures() == 0
+        env.close()
+
+
+def test_retrim_first_reset_uses_mean_wind(torch):
+    """Before its first step an env's last wind is the mean wind (helicopter.py:55): the re-trimmed
+    reset equals the template trim."""
+    env = make_env(torch, 130, "hover", 0.01, autoreset=True, reset_mode="retrim")
+    obs, _ = env.reset()
+    st, _ = env.get_state()
+    torch.cuda.synchronize()
+    tr = env.template()
+    err_s = np.abs(st.cpu().numpy()[:, :18] - tr["state"]) / (np.abs(tr["state"]) + 1)
+    err_o = np.abs(obs.cpu().numpy() - tr["obs"]) / (np.abs(tr["obs"]) + 1)
+    print(f"\n[retrim first reset vs template] state {err_s.max():.2e} obs {err_o.max():.2e}")
+    assert err_s.max() <= 1e-5 and err_o.max() <= 1e-5
+    env.close()

@@ -16,8 +16,12 @@ trim.npz         Newton trim results (helicopter_dynamics.py:491-576) for severa
 traj_dt0.02.npz  per-step trajectories of `Heli.step` (helicopter.py:192-206) for
 traj_dt0.01.npz  scenarios covering every branch of the step (see SCENARIOS), with the
                  recorded turbulence noise `eta` so the step can be replayed exactly.
+reset_f8.npz     second-episode resets (F8): the reference re-trims against the wind of the
+                 last step (helicopter.py:198, helicopter_dynamics.py:66-71,491-555) -- winds,
+                 reset states for several trim conditions / dt, and terminal steps of episodes
+                 that end by a crash followed by the reset the reference computes.
 
-Usage: python tools/gen_goldens.py   (numpy 2.2.6 promotion rules are part of the result)
+Usage: python tools/gen_goldens.py [--only f8]   (numpy 2.2.6 promotion rules are part of the result)
 """
 import json
 import os
@@ -190,6 +194,93 @@ def gen_trim(ns):
     return out
 
 
+F8_CASES = [  # (dt, trim overrides, steps before the reset, action kind, seed)
+    (0.02, {}, 50, "zero", 11),
+    (0.02, {}, 300, "trim_noise", 12),
+    (0.01, {}, 120, "trim_noise", 13),
+    (0.01, {"gr_alt": 1500.0}, 200, "trim_noise", 14),
+    (0.02, {"gr_alt": 2500.0}, 150, "trim_noise", 15),
+    (0.02, {"ned_vel": [80.0, 0.0, 0.0]}, 100, "trim_noise", 16),
+    (0.01, {"yaw_rate": 0.1, "yaw": 1.0}, 80, "trim_noise", 17),
+    (0.01, {}, 400, "uniform", 18),
+]
+
+
+def _action(kind, trim_a, arng):
+    if kind == "zero":
+        return np.zeros(4, np.float32)
+    if kind == "uniform":
+        return arng.uniform(-1, 1, size=4).astype(np.float32)
+    if kind == "trim_noise":
+        return (trim_a + arng.uniform(-0.05, 0.05, size=4)).astype(np.float32)
+    if kind == "low_collective":
+        a = trim_a.copy()
+        a[0] = -1.0
+        a[1:] += arng.uniform(-0.02, 0.02, size=3).astype(np.float32)
+        return a
+    raise ValueError(kind)
+
+
+def gen_f8(ns):
+    out = {}
+    rows = {k: [] for k in ["dt", "cond", "wind_ned", "state", "action", "obs"]}
+    for dt, cond, steps, kind, seed in F8_CASES:
+        env = make_env(ns, dt)
+        env.set_trim_cond(cond)
+        np.random.seed(seed)
+        arng = np.random.RandomState(seed + 1000)
+        env.reset()
+        trim_a = np.asarray(env.heli_dyn.action, dtype=np.float32)
+        for _ in range(steps):
+            _, _, term, trunc, _ = env.step(_action(kind, trim_a, arng))
+            if term or trunc:
+                break
+        w = np.asarray(env.heli_dyn.WIND_NED, dtype=np.float64)
+        obs2, _ = env.reset()
+        rows["dt"].append(dt)
+        rows["cond"].append(trim_vec(cond))
+        rows["wind_ned"].append(w)
+        rows["state"].append(np.asarray(env.heli_dyn.state.val, dtype=np.float64))
+        rows["action"].append(np.asarray(env.heli_dyn.action, dtype=np.float64))
+        rows["obs"].append(np.asarray(obs2, dtype=np.float64))
+    out.update({f"case/{k}": np.array(v) for k, v in rows.items()})
+    # Episodes that end by a crash, then reset: the terminal step's inputs and the reset result.
+    ep = {k: [] for k in ["dt", "t", "succ_before", "pre_state", "pre_wind", "pre_obs", "action", "eta",
+                          "wind_ned", "failed", "reset_state", "reset_obs", "reset_action"]}
+    for dt, seed in [(0.02, 21), (0.01, 22), (0.01, 23)]:
+        env = make_env(ns, dt)
+        np.random.seed(seed)
+        arng = np.random.RandomState(seed + 1000)
+        obs, _ = env.reset()
+        trim_a = np.asarray(env.heli_dyn.action, dtype=np.float32)
+        succ = 0
+        for t in range(3000):
+            pre = (np.asarray(env.heli_dyn.state.val, dtype=np.float64),
+                   np.asarray(env.wind_dyn.state.val, dtype=np.float64), np.asarray(obs, dtype=np.float64))
+            a = _action("low_collective", trim_a, arng)
+            obs, _, term, trunc, info = env.step(a)
+            _, shv = ns.tasks.HeliHover._calculate_reward(env)
+            if term or trunc:
+                ep["dt"].append(dt)
+                ep["t"].append(t)
+                ep["succ_before"].append(succ)
+                ep["pre_state"].append(pre[0])
+                ep["pre_wind"].append(pre[1])
+                ep["pre_obs"].append(pre[2])
+                ep["action"].append(a.astype(np.float64))
+                ep["eta"].append(np.asarray(env.wind_dyn.eta, dtype=np.float64))
+                ep["wind_ned"].append(np.asarray(env.heli_dyn.WIND_NED, dtype=np.float64))
+                ep["failed"].append(bool(info["failed"]))
+                obs2, _ = env.reset()
+                ep["reset_state"].append(np.asarray(env.heli_dyn.state.val, dtype=np.float64))
+                ep["reset_obs"].append(np.asarray(obs2, dtype=np.float64))
+                ep["reset_action"].append(np.asarray(env.heli_dyn.action, dtype=np.float64))
+                break
+            succ += int(bool(shv))
+    out.update({f"episode/{k}": np.array(v) for k, v in ep.items()})
+    return out
+
+
 def run_scenario(ns, dt, name, cond, kind, max_steps, seed):
     env = make_env(ns, dt)
     env.set_trim_cond(cond)
@@ -253,6 +344,11 @@ def run_scenario(ns, dt, name, cond, kind, max_steps, seed):
 def main():
     os.makedirs(OUT, exist_ok=True)
     ns = refload.load()
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
+    if only in (None, "f8"):
+        np.savez_compressed(os.path.join(OUT, "reset_f8.npz"), **gen_f8(ns))
+    if only is not None:
+        return
     meta = {"numpy": np.__version__, "generator": "tools/gen_goldens.py",
             "reference": "ugurcanozalp/heli-gym v2 (/root/reference)"}
     np.savez_compressed(os.path.join(OUT, "kats.npz"), **gen_kats(ns))
