@@ -265,7 +265,7 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
 #pragma unroll
     for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
     TSTAMP(8, "v"(hs[8]), "v"(hs[11]), "v"(obs[16]));
-    if (P.reset_retrim && active) {   // F8: a reset this step is trimmed against this wind
+    if (P.reset_retrim && active && !(P.autoreset_next && step < 0)) {   // F8: a reset trims against this wind
         float* wb = a.retrim_wind + 3 * blk0;
         st_lane<false>(wb + 0, 3 * (uint32_t)tid, W[0]);
         st_lane<false>(wb + 1, 3 * (uint32_t)tid, W[1]);
@@ -294,21 +294,24 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     TSTAMP(9, "v"(rew), "v"((int)failed));
     const bool successed = succ >= P.success_steps;   // successed_time before this step's add
     const bool time_up = step >= P.time_up_steps;
-    const bool term = failed || successed;
-    const bool done = term || time_up;
+    // next-step auto-reset: an env that ended last step (counter -1) only resets this step
+    const bool pending = P.autoreset_next && step == 0;
+    const bool term = (failed || successed) && !pending;
+    const bool trunc = (time_up || step >= P.max_episode_steps) && !pending;   // + TimeLimit
+    const bool done = term || trunc;
     succ += success_step ? 1 : 0;
 
     if (active) {
-        st_lane<NT>(a.reward + blk0, (uint32_t)tid, rew);
+        st_lane<NT>(a.reward + blk0, (uint32_t)tid, pending ? 0.f : rew);
         st_lane<NT>(a.terminated + blk0, (uint32_t)tid, (uint8_t)term);
-        st_lane<NT>(a.truncated + blk0, (uint32_t)tid, (uint8_t)time_up);
+        st_lane<NT>(a.truncated + blk0, (uint32_t)tid, (uint8_t)trunc);
         if (a.info)
-            st_lane<NT>(a.info + blk0, (uint32_t)tid, (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
+            st_lane<NT>(a.info + blk0, (uint32_t)tid, pending ? (uint8_t)0 : (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
                                   (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0)));
     }
 
-    // same-step auto-reset with a wave-ballot compaction of the finished envs
-    const bool do_reset = P.autoreset && active && done;
+    // auto-reset (same step, or the step after the end) with a wave-ballot compaction
+    const bool do_reset = P.autoreset && active && (P.autoreset_next ? pending : done);
     if (P.autoreset && a.reset_count) {
         const unsigned long long mask = __ballot(do_reset);
         if (mask) {
@@ -354,6 +357,7 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
         carry[1] = obs[5];
         carry[2] = obs[6];
         carry[3] = obs[16];
+        if (P.autoreset_next && done) step = -1;   // reset on the next step
     }
 
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
@@ -819,6 +823,9 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
     P.success_steps = first_step_above(dt, c.max_time / 4, false);
     P.autoreset = c.autoreset ? 1 : 0;
     P.reset_retrim = (c.autoreset && c.reset_mode == HG_RESET_RETRIM) ? 1 : 0;
+    P.autoreset_next = (c.autoreset && c.autoreset_mode == HG_AUTORESET_NEXT_STEP) ? 1 : 0;
+    P.max_episode_steps = (c.max_episode_steps > 0 && c.max_episode_steps < INT32_MAX) ? (int32_t)c.max_episode_steps
+                                                                                        : INT32_MAX;
     return P;
 }
 
@@ -898,6 +905,9 @@ int32_t check_config(const hg_config* c, int32_t rows, int32_t cols) {
     if (c->af.env_TURB_LVL < 0 || c->af.env_TURB_LVL > 7) return fail(HG_E_INVALID, "TURB_LVL must be 0..7");
     if (c->reset_mode != HG_RESET_TEMPLATE && c->reset_mode != HG_RESET_RETRIM)
         return fail(HG_E_INVALID, "reset_mode must be HG_RESET_TEMPLATE or HG_RESET_RETRIM");
+    if (c->autoreset_mode != HG_AUTORESET_SAME_STEP && c->autoreset_mode != HG_AUTORESET_NEXT_STEP)
+        return fail(HG_E_INVALID, "autoreset_mode must be HG_AUTORESET_SAME_STEP or HG_AUTORESET_NEXT_STEP");
+    if (c->max_episode_steps < 0) return fail(HG_E_INVALID, "max_episode_steps must be >= 0");
     if (rows < 2 || cols < 2 || rows != cols)
         return fail(HG_E_INVALID, "terrain must be a square map of at least 2x2 samples");
     return HG_OK;

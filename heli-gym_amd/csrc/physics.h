@@ -169,6 +169,7 @@ struct Params {
     R n_t, n_t2, inv_n_x, inv_n_v, inv_n_a, tgt_n[3], vel_tgt_n, dwn_tgt_n;
     R fail_zdot, fail_ang;
     int32_t task, time_up_steps, success_steps, autoreset, reset_retrim;
+    int32_t autoreset_next, max_episode_steps;   // next-step auto-reset; TimeLimit (INT32_MAX: off)
 };
 
 // Reset template: trimmed heli state, zero turbulence state, carry and observation.

@@ -11,7 +11,25 @@ from .envs import Heli, HeliForwardFlight, HeliHover  # noqa: F401
 from .vector import OBS_NAMES, HeliVecEnv  # noqa: F401
 
 __all__ = ["Heli", "HeliHover", "HeliForwardFlight", "HeliVecEnv", "OBS_NAMES", "register_envs",
-           "HeliGymError"]
+           "make_vec", "HeliGymError"]
+
+# gymnasium ids of the reference registry (heligym/__init__.py:4-18) -> task
+ENV_IDS = {"Heli-v0": "heli", "HeliHover-v0": "hover", "HeliForwardFlight-v0": "forward_flight"}
+MAX_EPISODE_STEPS = 5000   # heligym/__init__.py:4-18
+REWARD_THRESHOLD = 0.95
+
+
+def make_vec(env_id, num_envs, autoreset_mode="next_step", max_episode_steps=MAX_EPISODE_STEPS, **kwargs):
+    """`gymnasium.make_vec(env_id, num_envs)` for the heligym ids: one batched GPU env with the
+    registry's TimeLimit (max_episode_steps=5000) and gymnasium's vector autoreset default
+    (next step); kwargs go to HeliVecEnv (dt, seed, device, reset_mode, trim_cond, ...)."""
+    if env_id not in ENV_IDS:
+        raise ValueError(f"unknown env id {env_id!r}; one of {sorted(ENV_IDS)}")
+    env = HeliVecEnv(num_envs, task=ENV_IDS[env_id], autoreset=True, autoreset_mode=autoreset_mode,
+                     max_episode_steps=max_episode_steps, **kwargs)
+    env.spec_id = env_id
+    env.reward_threshold = REWARD_THRESHOLD
+    return env
 
 
 def register_envs():
@@ -21,8 +39,13 @@ def register_envs():
         from gymnasium.envs.registration import register
     except ImportError:
         return False
+    import functools
     for name, cls in (("Heli-v0", "Heli"), ("HeliHover-v0", "HeliHover"),
                       ("HeliForwardFlight-v0", "HeliForwardFlight")):
-        register(id=name, entry_point=f"heligym_amd.envs:{cls}", max_episode_steps=5000,
-                 reward_threshold=0.95, nondeterministic=False)
+        kw = dict(id=name, entry_point=f"heligym_amd.envs:{cls}", max_episode_steps=MAX_EPISODE_STEPS,
+                  reward_threshold=REWARD_THRESHOLD, nondeterministic=False)
+        try:
+            register(vector_entry_point=functools.partial(make_vec, name), **kw)
+        except TypeError:   # gymnasium < 1.0 has no vector entry points
+            register(**kw)
     return True

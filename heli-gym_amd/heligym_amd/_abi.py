@@ -23,6 +23,8 @@ HG_TASK_HELI, HG_TASK_HOVER, HG_TASK_FORWARD_FLIGHT = 0, 1, 2
 HG_INFO_FAILED, HG_INFO_SUCCESSED, HG_INFO_TIME_UP, HG_INFO_SUCCESS_STEP = 1, 2, 4, 8
 HG_RESET_TEMPLATE, HG_RESET_RETRIM = 0, 1
 RESET_MODES = {"template": HG_RESET_TEMPLATE, "retrim": HG_RESET_RETRIM}
+HG_AUTORESET_SAME_STEP, HG_AUTORESET_NEXT_STEP = 0, 1
+AUTORESET_MODES = {"same_step": HG_AUTORESET_SAME_STEP, "next_step": HG_AUTORESET_NEXT_STEP}
 HG_ABI_VERSION = 2
 
 AIRFRAME_FIELDS = (
@@ -63,7 +65,8 @@ class hg_config(ctypes.Structure):
                 ("dt", ctypes.c_double), ("max_time", ctypes.c_double),
                 ("task", ctypes.c_int32), ("autoreset", ctypes.c_int32),
                 ("seed", ctypes.c_uint64), ("env_offset", ctypes.c_int64),
-                ("reset_mode", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("reset_mode", ctypes.c_int32), ("autoreset_mode", ctypes.c_int32),
+                ("max_episode_steps", ctypes.c_int64)]
 
 
 class hg_trim_result(ctypes.Structure):

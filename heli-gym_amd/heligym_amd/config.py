@@ -74,7 +74,7 @@ def fill_target(tg, target):
 
 def make_config(task="hover", dt=DT, heli_name="aw109", max_time=None, target=None,
                 trim_cond=None, autoreset=True, seed=0, env_offset=0, turbulence_level=None,
-                reset_mode="template"):
+                reset_mode="template", autoreset_mode="same_step", max_episode_steps=None):
     doc = load_airframe(heli_name)
     cfg = _abi.hg_config()
     af = doc["airframe"]
@@ -100,4 +100,8 @@ def make_config(task="hover", dt=DT, heli_name="aw109", max_time=None, target=No
     if reset_mode not in _abi.RESET_MODES:
         raise ValueError(f"unknown reset_mode {reset_mode!r}; one of {sorted(_abi.RESET_MODES)}")
     cfg.reset_mode = _abi.RESET_MODES[reset_mode]
+    if autoreset_mode not in _abi.AUTORESET_MODES:
+        raise ValueError(f"unknown autoreset_mode {autoreset_mode!r}; one of {sorted(_abi.AUTORESET_MODES)}")
+    cfg.autoreset_mode = _abi.AUTORESET_MODES[autoreset_mode]
+    cfg.max_episode_steps = int(max_episode_steps or 0)
     return cfg, doc

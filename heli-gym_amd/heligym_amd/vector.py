@@ -62,7 +62,8 @@ class HeliVecEnv:
 
     def __init__(self, num_envs, task="hover", dt=config.DT, heli_name="aw109", seed=0, device=None,
                  autoreset=True, env_offset=0, max_time=None, target=None, trim_cond=None,
-                 turbulence_level=None, reset_mode="template"):
+                 turbulence_level=None, reset_mode="template", autoreset_mode="same_step",
+                 max_episode_steps=None):
         import torch
         self.torch = torch
         self.lib = _abi.load_library()
@@ -76,8 +77,11 @@ class HeliVecEnv:
         self.cfg, doc = config.make_config(task=task, dt=dt, heli_name=heli_name, max_time=max_time,
                                            target=target, trim_cond=trim_cond, autoreset=autoreset,
                                            seed=seed, env_offset=env_offset,
-                                           turbulence_level=turbulence_level, reset_mode=reset_mode)
+                                           turbulence_level=turbulence_level, reset_mode=reset_mode,
+                                           autoreset_mode=autoreset_mode, max_episode_steps=max_episode_steps)
         self.reset_mode = reset_mode
+        self.autoreset_mode = autoreset_mode
+        self.max_episode_steps = max_episode_steps
         u16 = config.load_terrain(doc)
         self.terrain_ft = config.terrain_ft(u16, self.cfg.af.env_MAX_GR_ALT)
         self._target = dict(config.DEFAULT_TARGETS[task])
@@ -157,7 +161,7 @@ class HeliVecEnv:
             if tuple(e.shape) != (self.num_envs, 3):
                 raise ValueError("eta must be [N, 3]")
         self._keep = (a, e)
-        rs = with_reset_info and self.autoreset
+        rs = with_reset_info and self.autoreset and self.autoreset_mode == "same_step"
         self._check(self.lib.hg_step(
             self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated_u8),
             _ptr(self.truncated_u8), _ptr(self.info_u8), _ptr(e),
@@ -174,7 +178,7 @@ class HeliVecEnv:
                 "successed": (bits & _abi.HG_INFO_SUCCESSED) != 0,
                 "time_up": (bits & _abi.HG_INFO_TIME_UP) != 0,
                 "success_step": (bits & _abi.HG_INFO_SUCCESS_STEP) != 0}
-        if self.autoreset:
+        if self.autoreset and self.autoreset_mode == "same_step":
             k = int(self.reset_count.item())
             idx = self.reset_index[:k].long()
             order = t.argsort(idx)

@@ -61,6 +61,15 @@ enum { HG_TASK_HELI = 0, HG_TASK_HOVER = 1, HG_TASK_FORWARD_FLIGHT = 2 };
  *                      last set_wind, helicopter.py:198 -> helicopter_dynamics.py:66-71,491-555). */
 enum { HG_RESET_TEMPLATE = 0, HG_RESET_RETRIM = 1 };
 
+/* When auto-reset envs restart (hg_config.autoreset_mode, with autoreset = 1).
+ *   HG_AUTORESET_SAME_STEP: the step that ends an episode returns the reset observation; the
+ *                           terminal one goes to final_obs_dev (gymnasium SAME_STEP / SB3 style).
+ *   HG_AUTORESET_NEXT_STEP: the ending step returns the terminal observation; the env's next step
+ *                           ignores its action and returns the reset observation with reward 0 and
+ *                           both flags false (gymnasium >= 1.0 vector default).  Between the two,
+ *                           the env's episode-step counter reads -1. */
+enum { HG_AUTORESET_SAME_STEP = 0, HG_AUTORESET_NEXT_STEP = 1 };
+
 /* info bit-field written per env by hg_step (helicopter.py:219-224). */
 enum { HG_INFO_FAILED = 1, HG_INFO_SUCCESSED = 2, HG_INFO_TIME_UP = 4, HG_INFO_SUCCESS_STEP = 8 };
 
@@ -110,7 +119,9 @@ typedef struct hg_config {
     uint64_t seed;        /* Philox key for the turbulence noise (wind_dynamics.py:49-52) */
     int64_t env_offset;   /* global id of local env 0 (sharding: results independent of rank count) */
     int32_t reset_mode;   /* HG_RESET_* */
-    int32_t reserved;
+    int32_t autoreset_mode; /* HG_AUTORESET_* */
+    int64_t max_episode_steps; /* > 0: also truncate at this many steps (gymnasium TimeLimit, the
+                                  registry's max_episode_steps=5000, heligym/__init__.py:4-18); 0: off */
 } hg_config;
 
 /* Reset template produced by the trim (host values). */
