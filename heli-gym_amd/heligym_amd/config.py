@@ -32,19 +32,74 @@ DEFAULT_TARGETS = {
 TARGET_KEYS = ("north_loc", "east_loc", "sea_alt", "heading", "vel")
 
 
-def load_airframe(heli_name="aw109"):
-    path = os.path.join(_HERE, "helis", heli_name + ".yaml")
-    with open(path) as f:
-        doc = yaml.safe_load(f)
+# The reference's airframe schema (heligym/envs/helis/aw109.yaml): ENV / HELI sections, rotor and
+# surface sub-sections under HELI.  Keys map onto the flat hg_airframe names used here.
+_REF_ENV_KEYS = {"R": "env_R", "T0": "env_T0", "LAPSE": "env_LAPSE", "RO_SEA": "env_RO_SEA",
+                 "GRAV": "env_GRAV", "MAX_GR_ALT": "env_MAX_GR_ALT", "NS_MAX": "env_NS_MAX",
+                 "EW_MAX": "env_EW_MAX", "WIND_DIR": "env_WIND_DIR_deg", "WIND_SPD": "env_WIND_SPD",
+                 "TURB_LVL": "env_TURB_LVL"}
+_REF_SECTIONS = {"MR": "mr_", "TR": "tr_", "FUS": "fus_", "HT": "ht_", "VT": "vt_", "WN": "wn_", "LG": "lg_"}
+BUNDLED_TERRAIN = "assets/terrain_hmap_u16.npz"
+
+
+def airframe_from_reference_schema(ref, resource_dir=None):
+    """Convert a parameter document in the reference's schema (helicopter.py:49-54 loads it;
+    ENV, HELI and HELI.{MR,TR,FUS,HT,VT,WN,LG}) into this package's {"airframe", "terrain"} doc.
+    The terrain is ENV.HMAP_PATH under `resource_dir` (the reference's HELIGYM_RESOURCE_DIR,
+    helicopter_dynamics.py:39); the reference's own map resolves to the bundled derived copy."""
+    env, heli = ref["ENV"], ref["HELI"]
+    af = {dst: env[src] for src, dst in _REF_ENV_KEYS.items()}
+    for k, v in heli.items():
+        if k in _REF_SECTIONS:
+            af.update({_REF_SECTIONS[k] + kk: vv for kk, vv in v.items()})
+        else:
+            af[k] = v
+    missing = [n for n in _abi.AIRFRAME_FIELDS[0] + _abi.AIRFRAME_FIELDS[1] + ["env_TURB_LVL"] if n not in af]
+    if missing:
+        raise ValueError(f"airframe document lacks {missing}")
+    terrain = {"file": BUNDLED_TERRAIN}
+    hmap = env.get("HMAP_PATH")
+    if hmap:
+        root = resource_dir if resource_dir is not None else os.environ.get("HELIGYM_RESOURCE_DIR", "")
+        path = root + hmap
+        if os.path.exists(path):
+            terrain = {"file": path}
+        elif os.path.basename(hmap) != "terrain_hmap.png":
+            raise FileNotFoundError(f"terrain {path} not found (set HELIGYM_RESOURCE_DIR)")
+    return {"airframe": af, "terrain": terrain}
+
+
+def load_airframe(heli_name="aw109", resource_dir=None):
+    """Parameter document for `heli_name`: a bundled airframe ("aw109", helis/<name>.yaml), or a
+    path to a YAML file in either this package's schema or the reference's (helis/aw109.yaml)."""
+    if isinstance(heli_name, dict):
+        doc = heli_name
+    else:
+        path = heli_name if heli_name.endswith((".yaml", ".yml")) else os.path.join(_HERE, "helis", heli_name + ".yaml")
+        with open(path) as f:
+            doc = yaml.safe_load(f)
+    if "ENV" in doc and "HELI" in doc:
+        doc = airframe_from_reference_schema(doc, resource_dir)
     return doc
 
 
+def read_terrain(path):
+    """uint16 [rows, cols] height samples from a .npz (key "hmap") or a 16-bit grayscale PNG."""
+    if path.endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            return np.ascontiguousarray(z["hmap"], dtype=np.uint16)
+    from PIL import Image
+    with Image.open(path) as im:
+        a = np.asarray(im)
+    if a.ndim == 3:
+        a = a[..., 0]
+    return np.ascontiguousarray(a, dtype=np.uint16)
+
+
 def load_terrain(doc):
-    """uint16 [rows, cols] samples and their scale to ft (helicopter_dynamics.py:39-43)."""
-    path = os.path.join(_HERE, doc["terrain"]["file"])
-    with np.load(path, allow_pickle=False) as z:
-        u16 = np.ascontiguousarray(z["hmap"], dtype=np.uint16)
-    return u16
+    """uint16 [rows, cols] samples of the document's terrain (helicopter_dynamics.py:39-43)."""
+    f = doc["terrain"]["file"]
+    return read_terrain(f if os.path.isabs(f) else os.path.join(_HERE, f))
 
 
 def terrain_ft(u16, max_gr_alt):

@@ -63,7 +63,7 @@ class HeliVecEnv:
     def __init__(self, num_envs, task="hover", dt=config.DT, heli_name="aw109", seed=0, device=None,
                  autoreset=True, env_offset=0, max_time=None, target=None, trim_cond=None,
                  turbulence_level=None, reset_mode="template", autoreset_mode="same_step",
-                 max_episode_steps=None):
+                 max_episode_steps=None, terrain=None):
         import torch
         self.torch = torch
         self.lib = _abi.load_library()
@@ -82,8 +82,16 @@ class HeliVecEnv:
         self.reset_mode = reset_mode
         self.autoreset_mode = autoreset_mode
         self.max_episode_steps = max_episode_steps
-        u16 = config.load_terrain(doc)
-        self.terrain_ft = config.terrain_ft(u16, self.cfg.af.env_MAX_GR_ALT)
+        # terrain: the airframe document's map, or a path / uint16 samples / float heights in ft
+        if terrain is None or isinstance(terrain, str):
+            u16 = config.load_terrain(doc) if terrain is None else config.read_terrain(terrain)
+            self.terrain_ft = config.terrain_ft(u16, self.cfg.af.env_MAX_GR_ALT)
+        else:
+            t = np.asarray(terrain)
+            self.terrain_ft = (config.terrain_ft(t, self.cfg.af.env_MAX_GR_ALT) if t.dtype == np.uint16
+                               else np.ascontiguousarray(t, dtype=np.float64))
+        if self.terrain_ft.ndim != 2:
+            raise ValueError("terrain must be a 2-D map")
         self._target = dict(config.DEFAULT_TARGETS[task])
         self._target.update(target or {})
         self._trim_cond = config.fill_trim(_abi.hg_trim_cond(), trim_cond)
