@@ -164,9 +164,11 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
 #endif
 
 // TASK: reward / success of the task; ETA: noise injected by the caller (else in-kernel Philox);
-// NT: streaming output stores (see st_out).  All compile-time, so the hot kernel has no
-// data-independent branches to merge around.
-template <int TASK, bool ETA, bool NT>
+// NT: streaming output stores (see st_out); FEAT: the optional features (reset-info compaction,
+// per-reset re-trim, next-step auto-reset, TimeLimit) -- without them the kernel carries none of
+// their registers.  All compile-time, so the hot kernel has no data-independent branches to merge
+// around.
+template <int TASK, bool ETA, bool NT, bool FEAT>
 __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
     __shared__ float s_obs[kBlock * HG_N_OBS];
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
 #pragma unroll
     for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
     TSTAMP(8, "v"(hs[8]), "v"(hs[11]), "v"(obs[16]));
-    if (P.reset_retrim && active && !(P.autoreset_next && step < 0)) {   // F8: a reset trims against this wind
+    if (FEAT && P.reset_retrim && active && !(P.autoreset_next && step < 0)) {   // F8: a reset trims against this wind
         float* wb = a.retrim_wind + 3 * blk0;
         st_lane<false>(wb + 0, 3 * (uint32_t)tid, W[0]);
         st_lane<false>(wb + 1, 3 * (uint32_t)tid, W[1]);
@@ -295,9 +297,9 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     const bool successed = succ >= P.success_steps;   // successed_time before this step's add
     const bool time_up = step >= P.time_up_steps;
     // next-step auto-reset: an env that ended last step (counter -1) only resets this step
-    const bool pending = P.autoreset_next && step == 0;
+    const bool pending = FEAT && P.autoreset_next && step == 0;
     const bool term = (failed || successed) && !pending;
-    const bool trunc = (time_up || step >= P.max_episode_steps) && !pending;   // + TimeLimit
+    const bool trunc = (time_up || (FEAT && step >= P.max_episode_steps)) && !pending;   // + TimeLimit
     const bool done = term || trunc;
     succ += success_step ? 1 : 0;
 
@@ -311,8 +313,8 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     }
 
     // auto-reset (same step, or the step after the end) with a wave-ballot compaction
-    const bool do_reset = P.autoreset && active && (P.autoreset_next ? pending : done);
-    if (P.autoreset && a.reset_count) {
+    const bool do_reset = P.autoreset && active && ((FEAT && P.autoreset_next) ? pending : done);
+    if (FEAT && P.autoreset && a.reset_count) {
         const unsigned long long mask = __ballot(do_reset);
         if (mask) {
             const int leader = __ffsll((long long)mask) - 1;
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
             }
         }
     }
-    if (P.reset_retrim) {   // queue the resets for retrim_kernel (which overwrites the template)
+    if (FEAT && P.reset_retrim) {   // queue the resets for retrim_kernel (which overwrites the template)
         const unsigned long long mask = __ballot(do_reset);
         if (mask) {
             const int leader = __ffsll((long long)mask) - 1;
@@ -357,7 +359,7 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
         carry[1] = obs[5];
         carry[2] = obs[6];
         carry[3] = obs[16];
-        if (P.autoreset_next && done) step = -1;   // reset on the next step
+        if (FEAT && P.autoreset_next && done) step = -1;   // reset on the next step
     }
 
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
@@ -1223,10 +1225,16 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;
     const dim3 grid(grid_for(e->n)), block(kBlock);
-#define HG_LAUNCH_STEP_NT(T, NT)                                                                           \
-    do {                                                                                                   \
-        if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-        else hipLaunchKernelGGL((step_kernel<T, false, NT>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+    const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX;
+#define HG_LAUNCH_STEP_NT(T, NT)                                                                                 \
+    do {                                                                                                         \
+        if (feat) {                                                                                              \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+        } else {                                                                                                 \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+        }                                                                                                        \
     } while (0)
 #define HG_LAUNCH_STEP(T)                                   \
     do {                                                    \
