@@ -27,6 +27,9 @@ for p in (ROOT, os.path.join(ROOT, "heli-gym_amd"), os.path.join(ROOT, "tests"))
 # action 16 = 136 B; writes state 108 + counters 12 + obs 68 + reward 4 + terminated/truncated/info 3
 # = 195 B.
 BYTES_PER_ENV_STEP = 136 + 195
+# hg_rollout: per step action 16 + obs 68 + reward 4 + flags 3; state + counters (240 B) once per launch
+ROLLOUT_BYTES_PER_ENV_STEP = 16 + 68 + 4 + 3
+BYTES_STATE_RW = 2 * (108 + 12)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
 
 
@@ -38,6 +41,8 @@ def parse():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--dt", type=float, default=0.01)
     ap.add_argument("--task", default="hover", choices=["hover", "forward_flight", "heli"])
+    ap.add_argument("--rollout-steps", type=int, default=100,
+                    help="also time hg_rollout (this many steps per launch, same action bank); 0 = off")
     ap.add_argument("--reset-mode", default="template", choices=["template", "retrim"],
                     help="auto-reset state: mean-wind trim template (default) or per-reset device re-trim (F8)")
     ap.add_argument("--graph-steps", type=int, default=100, help="steps captured per hipGraph")
@@ -191,6 +196,34 @@ def main():
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     elapsed = float(el_t[0])
 
+    # Secondary figure (not `value`): the same workload as open-loop rollouts, hg_rollout over the
+    # same action bank, `rollout_steps` steps per launch with the env state kept in registers.
+    roll = None
+    if args.rollout_steps > 0 and gathered is None and args.reset_mode == "template":
+        R = args.rollout_steps
+        rbank = bank if R == B else torch.stack([bank[k % B] for k in range(R)])
+        rout = env.rollout(rbank)
+        torch.cuda.synchronize()
+        nroll = max(1, K // R)
+        if world > 1:
+            dist.barrier()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record()
+        for _ in range(nroll):
+            env.rollout(rbank, out=rout)
+        r1.record()
+        torch.cuda.synchronize()
+        rt = torch.tensor([r0.elapsed_time(r1) * 1e-3], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(rt, op=dist.ReduceOp.MAX)
+        rsec = float(rt[0])
+        roll = {"api": "hg_rollout", "steps_per_launch": R, "steps": nroll * R,
+                "value": N * world * nroll * R / rsec, "unit": "env-steps/s",
+                "ms_per_step": rsec / (nroll * R) * 1e3,
+                "bytes_per_env_step": ROLLOUT_BYTES_PER_ENV_STEP + BYTES_STATE_RW / R,
+                "note": "open-loop action sequences (planning / data generation); same results as "
+                        "hg_step, state read and written once per launch"}
+
     # Average step-kernel duration = HIP-event time of the timed region / launches: in graph mode
     # the region holds exactly K step-kernel launches back to back on the env's stream (no other
     # work), which is what rocprofv3's kernel-trace average measures (profiles/*_kernel_stats.csv).
@@ -232,6 +265,8 @@ def main():
                      "algorithmic_bytes_per_launch": N * BYTES_PER_ENV_STEP},
         "wall_s": float(el_t[1]),
     }
+    if roll is not None:
+        out["rollout"] = roll
     tr = pmc_traffic(N, args.dt, args.task)
     if tr is not None:
         out["roofline"]["traffic"] = tr[0]

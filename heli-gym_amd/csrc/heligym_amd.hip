@@ -92,6 +92,7 @@ struct StepArgs {
     float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
     int32_t* retrim_list;    // ... compacted ids of the envs to re-trim
     int32_t* retrim_count;   // ... their number (zeroed before the launch)
+    int32_t nsteps;          // MULTI: steps per launch (inputs / outputs stacked [nsteps][N])
     int64_t n;
     uint64_t seed;
     int64_t env_offset;
@@ -166,9 +167,10 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
 // TASK: reward / success of the task; ETA: noise injected by the caller (else in-kernel Philox);
 // NT: streaming output stores (see st_out); FEAT: the optional features (reset-info compaction,
 // per-reset re-trim, next-step auto-reset, TimeLimit) -- without them the kernel carries none of
-// their registers.  All compile-time, so the hot kernel has no data-independent branches to merge
-// around.
-template <int TASK, bool ETA, bool NT, bool FEAT>
+// their registers; MULTI: a.nsteps consecutive steps per launch (hg_rollout) with the env state
+// kept in registers between them.  All compile-time, so the hot kernel has no data-independent
+// branches to merge around.
+template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI>
 __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
     __shared__ float s_obs[kBlock * HG_N_OBS];
@@ -211,7 +213,10 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lo);
 #pragma unroll
     for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lo);
-    const float4 act = ld_lane(reinterpret_cast<const float4*>(a.actions) + blk0, lo);
+    const int nsteps = MULTI ? a.nsteps : 1;
+    for (int sstep = 0; sstep < nsteps; ++sstep) {
+    const int64_t so = MULTI ? (int64_t)sstep * n : 0;   // first row of this step's inputs / outputs
+    const float4 act = ld_lane(reinterpret_cast<const float4*>(a.actions) + so + blk0, lo);
     const int lane = tid & 63;
     // terrain texels under the committed position (F6): issued now, combined after the wind step
     const hg::GroundCell<float> cell_c = hg::ground_cell(P, hs[15], hs[16]);
@@ -221,7 +226,7 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
     float eta[3];
     if (ETA) {
-        const float* eb = a.eta + 3 * blk0;
+        const float* eb = a.eta + 3 * (so + blk0);
         eta[0] = ld_lane(eb + 0, 3 * lo);
         eta[1] = ld_lane(eb + 1, 3 * lo);
         eta[2] = ld_lane(eb + 2, 3 * lo);
@@ -304,11 +309,11 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     succ += success_step ? 1 : 0;
 
     if (active) {
-        st_lane<NT>(a.reward + blk0, (uint32_t)tid, pending ? 0.f : rew);
-        st_lane<NT>(a.terminated + blk0, (uint32_t)tid, (uint8_t)term);
-        st_lane<NT>(a.truncated + blk0, (uint32_t)tid, (uint8_t)trunc);
+        st_lane<NT>(a.reward + so + blk0, (uint32_t)tid, pending ? 0.f : rew);
+        st_lane<NT>(a.terminated + so + blk0, (uint32_t)tid, (uint8_t)term);
+        st_lane<NT>(a.truncated + so + blk0, (uint32_t)tid, (uint8_t)trunc);
         if (a.info)
-            st_lane<NT>(a.info + blk0, (uint32_t)tid, pending ? (uint8_t)0 : (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
+            st_lane<NT>(a.info + so + blk0, (uint32_t)tid, pending ? (uint8_t)0 : (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
                                   (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0)));
     }
 
@@ -362,6 +367,23 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
         if (FEAT && P.autoreset_next && done) step = -1;   // reset on the next step
     }
 
+    TSTAMP(10, "v"(hs[0]));
+    // observations: stage through LDS (stride 17 is bank-conflict free) -> contiguous float4 stores
+    // observations: each wave stages its 64 rows in its own LDS slice (stride 17 is bank-conflict
+    // free) and writes them back as contiguous float4, with no block-wide barrier
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
+    float* w_obs = s_obs + wv * 64 * HG_N_OBS;
+#pragma unroll
+    for (int c = 0; c < 17; ++c) w_obs[lane * 17 + c] = obs[c];
+    __builtin_amdgcn_wave_barrier();
+    const int64_t w0 = blk0 + wv * 64;
+    const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
+    const int cnt = nw > 0 ? nw * 17 : 0;
+    float* out = a.obs + (so + w0) * 17;
+    const int n4 = cnt >> 2;
+    for (int j = lane; j < n4; j += 64) st_out4<NT>(out + 4 * j, w_obs + 4 * j);
+    for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
+    }   // steps
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
     st_b = a.state + blk0;
     ct_b = a.counters + blk0;
@@ -378,22 +400,6 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
         st_lane<NT>(COL(ct_b, 2), (uint32_t)tid, epi);
     }
 
-    TSTAMP(10, "v"(hs[0]));
-    // observations: stage through LDS (stride 17 is bank-conflict free) -> contiguous float4 stores
-    // observations: each wave stages its 64 rows in its own LDS slice (stride 17 is bank-conflict
-    // free) and writes them back as contiguous float4, with no block-wide barrier
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
-    float* w_obs = s_obs + wv * 64 * HG_N_OBS;
-#pragma unroll
-    for (int c = 0; c < 17; ++c) w_obs[lane * 17 + c] = obs[c];
-    __builtin_amdgcn_wave_barrier();
-    const int64_t w0 = blk0 + wv * 64;
-    const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
-    const int cnt = nw > 0 ? nw * 17 : 0;
-    float* out = a.obs + w0 * 17;
-    const int n4 = cnt >> 2;
-    for (int j = lane; j < n4; j += 64) st_out4<NT>(out + 4 * j, w_obs + 4 * j);
-    for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
     TSTAMP(11, "v"(tid));
 #if HG_TIMING
     __builtin_amdgcn_s_waitcnt(0);
@@ -1221,6 +1227,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     a.retrim_wind = e->retrim_wind;
     a.retrim_list = e->retrim_list;
     a.retrim_count = e->retrim_count;
+    a.nsteps = 1;
     a.n = e->n;
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;
@@ -1229,11 +1236,11 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
 #define HG_LAUNCH_STEP_NT(T, NT)                                                                                 \
     do {                                                                                                         \
         if (feat) {                                                                                              \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
         } else {                                                                                                 \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
         }                                                                                                        \
     } while (0)
 #define HG_LAUNCH_STEP(T)                                   \
@@ -1263,6 +1270,61 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
         hipLaunchKernelGGL(retrim_kernel, dim3(retrim_grid(e->n)), dim3(64), 0, s, r);
     }
 #undef HG_LAUNCH_STEP
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, float* reward, uint8_t* terminated,
+                   uint8_t* truncated, uint8_t* info, const float* eta, void* stream) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    if (nsteps < 1) return fail(HG_E_INVALID, "nsteps must be >= 1");
+    if (!actions || !obs || !reward || !terminated || !truncated)
+        return fail(HG_E_INVALID, "actions/obs/reward/terminated/truncated must be device pointers");
+    if (((uintptr_t)actions & 15) || ((uintptr_t)obs & 15))
+        return fail(HG_E_INVALID, "actions and obs must be 16-byte aligned");
+    if (e->Pf.reset_retrim)
+        return fail(HG_E_INVALID, "hg_rollout does not support reset_mode RETRIM (re-trims run between steps)");
+    StepArgs a;
+    memset(&a, 0, sizeof(a));
+    a.state = e->state;
+    a.counters = e->counters;
+    a.hmap = e->hmap;
+    a.actions = actions;
+    a.obs = obs;
+    a.reward = reward;
+    a.terminated = terminated;
+    a.truncated = truncated;
+    a.info = info;
+    a.eta = eta;
+    a.nsteps = nsteps;
+    a.n = e->n;
+    a.seed = e->cfg.seed;
+    a.env_offset = e->cfg.env_offset;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid(grid_for(e->n)), block(kBlock);
+    const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX;
+#define HG_LAUNCH_ROLL_NT(T, NT)                                                                                 \
+    do {                                                                                                         \
+        if (feat) {                                                                                              \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+        } else {                                                                                                 \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+        }                                                                                                        \
+    } while (0)
+#define HG_LAUNCH_ROLL(T)                                   \
+    do {                                                    \
+        if (e->n <= e->resident_envs) HG_LAUNCH_ROLL_NT(T, true); \
+        else HG_LAUNCH_ROLL_NT(T, false);                   \
+    } while (0)
+    switch (e->cfg.task) {
+        case HG_TASK_HOVER: HG_LAUNCH_ROLL(HG_TASK_HOVER); break;
+        case HG_TASK_FORWARD_FLIGHT: HG_LAUNCH_ROLL(HG_TASK_FORWARD_FLIGHT); break;
+        default: HG_LAUNCH_ROLL(HG_TASK_HELI); break;
+    }
+#undef HG_LAUNCH_ROLL
+#undef HG_LAUNCH_ROLL_NT
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }

@@ -98,6 +98,7 @@ _SIGS = {
     "hg_set_state": (ctypes.c_int32, [_P, _P, _P, _P]),
     "hg_random_actions": (ctypes.c_int32, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,
                                            ctypes.c_float, _P]),
+    "hg_rollout": (ctypes.c_int32, [_P, _P, ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P]),
     "hg_trim_batch": (ctypes.c_int32, [_P, _P, ctypes.c_int64, _P, _P, _P, _P, _P]),
     "hg_retrim_failures": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
 }

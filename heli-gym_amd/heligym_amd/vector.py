@@ -246,6 +246,35 @@ class HeliVecEnv:
         self._check(self.lib.hg_set_state(self._h, _ptr(s), _ptr(c), self._stream()))
         self._keep_state = (s, c)
 
+    def rollout(self, actions, eta=None, out=None):
+        """Open-loop rollout (hg_rollout): actions [K,N,4] applied over K consecutive steps in one
+        launch, identical to K step() calls.  Returns (obs [K,N,17], reward [K,N], terminated,
+        truncated [K,N] bool, info bits [K,N] uint8) device tensors (`out` buffers are reused if
+        given, as returned by a previous call)."""
+        t = self.torch
+        a = actions
+        if a.dtype != t.float32 or not a.is_contiguous() or a.device != self.device:
+            a = a.to(device=self.device, dtype=t.float32).contiguous()
+        if a.ndim != 3 or tuple(a.shape[1:]) != (self.num_envs, _abi.HG_N_ACT):
+            raise ValueError(f"actions must be [K, {self.num_envs}, 4], got {tuple(a.shape)}")
+        K, N = a.shape[0], self.num_envs
+        e = None
+        if eta is not None:
+            e = eta.to(device=self.device, dtype=t.float32).contiguous()
+            if tuple(e.shape) != (K, N, 3):
+                raise ValueError("eta must be [K, N, 3]")
+        if out is None or out[0].shape[0] != K:
+            out = (t.empty((K, N, _abi.HG_N_OBS), dtype=t.float32, device=self.device),
+                   t.empty((K, N), dtype=t.float32, device=self.device),
+                   t.empty((K, N), dtype=t.uint8, device=self.device),
+                   t.empty((K, N), dtype=t.uint8, device=self.device),
+                   t.empty((K, N), dtype=t.uint8, device=self.device))
+        obs, rew, term, trunc, info = out
+        self._keep = (a, e)
+        self._check(self.lib.hg_rollout(self._h, _ptr(a), K, _ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc),
+                                        _ptr(info), _ptr(e), self._stream()))
+        return out
+
     def trim_batch(self, wind_ned):
         """Device batched trim (hg_trim_batch) of this env's trim condition against each row of
         `wind_ned` [K,3] (ft/s NED): the reset the reference computes from its second episode on.

@@ -198,6 +198,17 @@ int32_t hg_step(hg_env* env, const float* actions_dev, float* obs_dev, float* re
                 const float* eta_dev, int32_t* reset_count_dev, int32_t* reset_index_dev,
                 float* final_obs_dev, void* stream);
 
+/* Open-loop rollout: `nsteps` consecutive hg_step calls in one launch, each env's state kept in
+ * registers between steps (state is read and written once).  Results are identical to nsteps
+ * hg_step calls with the same inputs (same auto-reset, noise keys, flags).  Inputs / outputs are
+ * stacked per step: actions_dev [nsteps,N,4], obs_dev [nsteps,N,17], reward_dev [nsteps,N],
+ * terminated_dev / truncated_dev / info_dev (or NULL) [nsteps,N], eta_dev [nsteps,N,3] or NULL.
+ * For action sequences fixed in advance (sampling-based planning, data generation, replay); no
+ * reset-info compaction; not available with HG_RESET_RETRIM. */
+int32_t hg_rollout(hg_env* env, const float* actions_dev, int32_t nsteps, float* obs_dev, float* reward_dev,
+                   uint8_t* terminated_dev, uint8_t* truncated_dev, uint8_t* info_dev, const float* eta_dev,
+                   void* stream);
+
 /* Batched device trim: HelicopterDynamics.trim (helicopter_dynamics.py:491-576) of the env's trim
  * condition against `count` winds at once — the reset path of reset_mode HG_RESET_RETRIM, exposed
  * for direct use.  Same Newton iteration as hg_trim (fp64, trial point rounded to fp32), with the

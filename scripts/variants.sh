@@ -13,5 +13,7 @@ python - <<'PY'
 import json
 for l in open("gpurun_out/variants.jsonl"):
     d = json.loads(l); r = d["roofline"]; p = d.get("max_abs_step_err") or {}
-    print(f'{d["variant"]} N={d["config"]["envs_per_gpu"]:8d} {d["value"]:.3e} steps/s {d["ms_per_step"]*1e3:7.1f} us/step kern {r["kernel_avg_us"]:7.1f} us frac {r["frac"]:.3f} err/tol {p.get("max_err_over_tol", -1):.3f}')
+    ro = d.get("rollout") or {}
+    print(f'{d["variant"]} N={d["config"]["envs_per_gpu"]:8d} {d["value"]:.3e} steps/s {d["ms_per_step"]*1e3:7.1f} us/step kern {r["kernel_avg_us"]:7.1f} us frac {r["frac"]:.3f} err/tol {p.get("max_err_over_tol", -1):.3f}'
+          f' | rollout {ro.get("value", 0):.3e} steps/s {ro.get("ms_per_step", 0)*1e3:6.1f} us/step')
 PY

@@ -563,3 +563,43 @@ def test_make_vec_registry_defaults(torch):
     assert env.task == "hover" and env.autoreset_mode == "next_step" and env.max_episode_steps == 5000
     assert env.cfg.max_episode_steps == 5000 and env.reward_threshold == 0.95
     env.close()
+
+
+@pytest.mark.parametrize("opts", [dict(), dict(eta=True), dict(max_episode_steps=37),
+                                  dict(autoreset_mode="next_step"), dict(task="forward_flight")])
+def test_rollout_equals_sequential_steps(torch, opts):
+    """hg_rollout (K steps per launch, state in registers) is bitwise identical to K hg_step calls:
+    observations, rewards, flags, info bits and the final state, across auto-resets."""
+    opts = dict(opts)
+    use_eta = opts.pop("eta", False)
+    task = opts.pop("task", "hover")
+    N, K = 1000, 200
+    outs = []
+    for mode in ("steps", "rollout"):
+        env = make_env(torch, N, task, 0.02, autoreset=True, seed=11, **opts)
+        env.reset()
+        acts = torch.empty((K, N, 4), dtype=torch.float32, device=env.device)
+        for k in range(K):
+            env.random_actions(acts[k], seed=2, step=k)
+        acts[:, : N // 2, 0] = -1.0   # low collective on half the envs: crashes and auto-resets
+        eta = None
+        if use_eta:
+            g = torch.Generator(device=env.device).manual_seed(3)
+            eta = torch.randn((K, N, 3), generator=g, device=env.device) * 7.0
+        if mode == "steps":
+            rec = [[] for _ in range(5)]
+            for k in range(K):
+                env.step_async(acts[k], eta=None if eta is None else eta[k], with_reset_info=False)
+                for lst, buf in zip(rec, (env.obs, env.reward, env.terminated_u8, env.truncated_u8, env.info_u8)):
+                    lst.append(buf.clone())
+            res = [torch.stack(r) for r in rec]
+        else:
+            res = list(env.rollout(acts, eta=eta))
+        st, ctr = env.get_state()
+        torch.cuda.synchronize()
+        outs.append([r.cpu().numpy() for r in res] + [st.cpu().numpy(), ctr.cpu().numpy()])
+        env.close()
+    n_done = int((outs[0][2] | outs[0][3]).sum())
+    assert n_done > 0
+    for x, y in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(x, y)
