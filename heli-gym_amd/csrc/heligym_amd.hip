@@ -8,8 +8,8 @@
 //   counters [HG_COUNTER_COLS][N] i32 SoA (episode step, success steps, episode index)
 //   actions  [N,4] fp32 (one float4 per lane)      obs [N,17] fp32 (LDS-staged, float4 stores)
 //   reward [N] fp32, terminated/truncated/info [N] u8
-// Model constants travel as the kernel argument (scalar registers); the terrain map (4 MiB fp32)
-// and the turbulence table stay cache-resident.
+// Model constants are read with scalar loads from a device copy; the terrain map (8 MiB float2
+// {hi, lo}) stays cache-resident.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -98,14 +98,9 @@ struct StepArgs {
     int64_t env_offset;
 };
 
-#ifndef HG_PARAMS_PTR
-#define HG_PARAMS_PTR 1
-#endif
-#if HG_PARAMS_PTR
+// Model constants travel as a pointer to a device copy (scalar loads); by value they would take
+// ~0.6 KB of kernel arguments and spill more SGPRs.
 using ParamArg = const Params<float>* __restrict__;
-#else
-using ParamArg = const Params<float>;
-#endif
 
 #ifndef HG_MIN_WAVES
 #define HG_MIN_WAVES 1
@@ -174,11 +169,7 @@ template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI>
 __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
     __shared__ float s_obs[kBlock * HG_N_OBS];
-#if HG_PARAMS_PTR
     const Params<float>& P = *Pa;   // model constants: scalar loads from a device copy
-#else
-    const Params<float>& P = Pa;
-#endif
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * kBlock;
     const int64_t i = blk0 + tid;
@@ -986,11 +977,7 @@ static inline unsigned retrim_grid(int64_t jobs) {
     return (unsigned)(jobs < 1 ? 1 : (jobs > 1024 ? 1024 : jobs));
 }
 
-#if HG_PARAMS_PTR
 #define PARAM_ARG(e) ((const Params<float>*)(e)->params_dev)
-#else
-#define PARAM_ARG(e) ((e)->Pf)
-#endif
 
 extern "C" {
 #if HG_TIMING

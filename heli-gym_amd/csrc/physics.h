@@ -30,13 +30,6 @@ HD double m_fmod(double x, double y) { return fmod(x, y); }
 // [-pi/4, pi/4]; ~1 ulp, ~25 VALU ops for both, no Payne-Hanek slow path (libm sincosf spills a
 // 36-byte scratch table for it).  Larger |x| keeps working with degrading absolute accuracy.
 HD void m_sincos(float x, float* s, float* c) {
-#if defined(HG_HW_SINCOS) && HG_HW_SINCOS && defined(__HIP_DEVICE_COMPILE__)
-    // v_sin_f32 / v_cos_f32 take revolutions
-    const float rv = x * 0.159154943091895336f;
-    *s = __builtin_amdgcn_sinf(rv);
-    *c = __builtin_amdgcn_cosf(rv);
-    return;
-#endif
     const float k = rintf(x * 0.636619772367581343f);
     float r = fmaf(k, -1.57079637050628662109375f, x);
     r = fmaf(k, 4.37113900018624283e-8f, r);
