@@ -129,6 +129,13 @@ __device__ __forceinline__ void st_out4(float* p, const float* s) {
     else *reinterpret_cast<f32x4*>(p) = v;
 }
 
+typedef __attribute__((address_space(4))) const Params<float> ConstParams;
+__device__ __forceinline__ const Params<float>* reload_params(const Params<float>* p) {
+    ConstParams* c = (ConstParams*)p;
+    asm volatile("" : "+s"(c));   // opaque: the loads cannot be hoisted out of the step loop
+    return (const Params<float>*)c;
+}
+
 // Per-lane access at a small byte offset from a uniform base (SGPR-base global load / store).
 template <typename T>
 __device__ __forceinline__ T ld_lane(const T* __restrict__ base, uint32_t idx) {
@@ -169,7 +176,7 @@ template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI>
 __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
     __shared__ float s_obs[kBlock * HG_N_OBS];
-    const Params<float>& P = *Pa;   // model constants: scalar loads from a device copy
+    const Params<float>& P0 = *Pa;   // model constants: scalar loads from a device copy
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * kBlock;
     const int64_t i = blk0 + tid;
@@ -206,6 +213,9 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lo);
     const int nsteps = MULTI ? a.nsteps : 1;
     for (int sstep = 0; sstep < nsteps; ++sstep) {
+    // MULTI: the constants are re-read (scalar cache) each step rather than kept live across the
+    // loop, where ~130 of them would spill out of the SGPR file
+    const Params<float>& P = MULTI ? *reload_params(Pa) : P0;
     const int64_t so = MULTI ? (int64_t)sstep * n : 0;   // first row of this step's inputs / outputs
     const float4 act = ld_lane(reinterpret_cast<const float4*>(a.actions) + so + blk0, lo);
     const int lane = tid & 63;
