@@ -4,8 +4,14 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
+
+# step_kernel<TASK, ETA, NT, FEAT, MULTI>: the per-step launch (MULTI false) is the judged kernel;
+# hg_rollout's multi-step launches (MULTI true) are summarised separately.
+SINGLE = re.compile(r"step_kernel<\d+(, (true|false)){2,3}(, false)?>")
+MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true>")
 
 d, tag, n, dt = sys.argv[1], sys.argv[2], int(sys.argv[3]), float(sys.argv[4])
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -14,19 +20,24 @@ os.makedirs(prof, exist_ok=True)
 stats = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
 if stats:
     shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-agg, durs = {}, []
+agg, durs, mdurs = {}, [], []
 for f in glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if "step_kernel" in r.get("Kernel_Name", ""):
+        if SINGLE.search(r.get("Kernel_Name", "")):
             agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
 for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        if "step_kernel" in r["Kernel_Name"]:
+        if SINGLE.search(r["Kernel_Name"]):
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        elif MULTI.search(r["Kernel_Name"]):
+            mdurs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
 out = {"tag": tag, "envs": n, "dt": dt, "kernel": "step_kernel<HOVER>",
        "kernel_avg_ns_trace": sum(durs) / len(durs) if durs else None,
        "launches_traced": len(durs), "counters_per_launch": mean}
+if mdurs:
+    out["rollout_kernel_avg_ns_trace"] = sum(mdurs) / len(mdurs)
+    out["rollout_launches_traced"] = len(mdurs)
 if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     # MI355X_MICROARCH.md HBM section: FETCH_SIZE/WRITE_SIZE are KiB; on gfx950 FETCH_SIZE reads
     # half the bytes of a coalesced streaming read (128-B requests tallied at 64 B) -> x2.
