@@ -146,6 +146,26 @@ __device__ __forceinline__ void st_lane(T* base, uint32_t idx, T v) {
     st_out<NT>(reinterpret_cast<T*>(reinterpret_cast<char*>(base) + idx * (uint32_t)sizeof(T)), v);
 }
 
+// Observations of a step: each wave stages its 64 rows in its own LDS slice (stride 17 is
+// bank-conflict free) and writes them back as contiguous float4, with no block-wide barrier.
+template <bool NT>
+__device__ __forceinline__ void store_obs(float* s_obs, const float obs[17], float* dst, int64_t so, int64_t blk0,
+                                          int64_t n, int tid) {
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
+    float* w_obs = s_obs + wv * 64 * HG_N_OBS;
+#pragma unroll
+    for (int c = 0; c < 17; ++c) w_obs[lane * 17 + c] = obs[c];
+    __builtin_amdgcn_wave_barrier();
+    const int64_t w0 = blk0 + wv * 64;
+    const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
+    const int cnt = nw > 0 ? nw * 17 : 0;
+    float* out = dst + (so + w0) * 17;
+    const int n4 = cnt >> 2;
+    for (int j = lane; j < n4; j += 64) st_out4<NT>(out + 4 * j, w_obs + 4 * j);
+    for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
+}
+
 // Diagnostic build only: per-wave phase timestamps (s_memtime) of one launch, for latency
 // attribution; lane 0 of each of the first HG_TIMING_WAVES waves records them.
 #ifndef HG_TIMING
@@ -197,20 +217,19 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
 #endif
     TSTAMP(0, "v"(tid));
     // Loads in the order they are needed: position (-> terrain texel address), counters (-> noise
-    // key), then the rest; the reset template is spread one float per lane (read back with
-    // readlane by resetting lanes) so a reset adds no memory round trip at the end of the step.
+    // key), wind state and carry (-> wind step), then the heli state.
     float hs[18], ws[5], carry[4];
     hs[15] = ld_lane(COL(st_b, 15), lo);
     hs[16] = ld_lane(COL(st_b, 16), lo);
     int32_t step = ld_lane(COL(ct_b, 0), lo), succ = ld_lane(COL(ct_b, 1), lo),
             epi = ld_lane(COL(ct_b, 2), lo);
 #pragma unroll
-    for (int c = 0; c < 18; ++c)
-        if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lo);
-#pragma unroll
-    for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lo);
+    for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lo);   // the wind step needs these
 #pragma unroll
     for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lo);
+#pragma unroll
+    for (int c = 0; c < 18; ++c)   // ... and the heli state streams in behind the noise and wind work
+        if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lo);
     const int nsteps = MULTI ? a.nsteps : 1;
     for (int sstep = 0; sstep < nsteps; ++sstep) {
     // MULTI: the constants are re-read (scalar cache) each step rather than kept live across the
@@ -291,6 +310,8 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     hs[13] = hg::pi_bound(hs[13]);
     hs[14] = hg::pi_bound(hs[14]);
 
+    TSTAMP(9, "v"(hs[0]));
+
     // reward (helicopter_with_tasks.py) and flags (helicopter.py:201-205, 219-240)
     bool success_step = false;
     float rew = 0.f;
@@ -299,7 +320,7 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
     step += 1;
     const bool failed = hg::is_failed(P, hs, k, h_post);
-    TSTAMP(9, "v"(rew), "v"((int)failed));
+    TSTAMP(10, "v"(rew), "v"((int)failed));
     const bool successed = succ >= P.success_steps;   // successed_time before this step's add
     const bool time_up = step >= P.time_up_steps;
     // next-step auto-reset: an env that ended last step (counter -1) only resets this step
@@ -367,23 +388,7 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
         carry[3] = obs[16];
         if (FEAT && P.autoreset_next && done) step = -1;   // reset on the next step
     }
-
-    TSTAMP(10, "v"(hs[0]));
-    // observations: stage through LDS (stride 17 is bank-conflict free) -> contiguous float4 stores
-    // observations: each wave stages its 64 rows in its own LDS slice (stride 17 is bank-conflict
-    // free) and writes them back as contiguous float4, with no block-wide barrier
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
-    float* w_obs = s_obs + wv * 64 * HG_N_OBS;
-#pragma unroll
-    for (int c = 0; c < 17; ++c) w_obs[lane * 17 + c] = obs[c];
-    __builtin_amdgcn_wave_barrier();
-    const int64_t w0 = blk0 + wv * 64;
-    const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
-    const int cnt = nw > 0 ? nw * 17 : 0;
-    float* out = a.obs + (so + w0) * 17;
-    const int n4 = cnt >> 2;
-    for (int j = lane; j < n4; j += 64) st_out4<NT>(out + 4 * j, w_obs + 4 * j);
-    for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
+    store_obs<NT>(s_obs, obs, a.obs, so, blk0, n, tid);
     }   // steps
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
     st_b = a.state + blk0;

@@ -12,8 +12,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "heli-gym_amd"))
 
 PHASES = ["state loads", "philox", "wind step", "ground h_c", "RK stage 1", "RK stage 2", "RK stage 3",
-          "RK stage 4", "reward+flags+ground", "flag stores+reset", "obs LDS+stores", "state stores",
-          "store drain"]
+          "RK stage 4 + update", "wraps + template fetch", "reward/flags/post-ground",
+          "flag stores + reset + obs stores", "state stores", "store drain"]
 ORDER = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 11, 12]   # stamp slots in program order
 
 
