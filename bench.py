@@ -71,7 +71,9 @@ def pmc_traffic(envs, dt, task):
 
 
 def cpu_baseline(dt, task, seconds):
-    """Oracle (C restatement, 1 thread) on a bounded sample of the same workload."""
+    """Oracle (C restatement) on a bounded sample of the same workload: one host core, then the
+    box's CPU share (OMP_NUM_THREADS threads, each stepping its own envs; ctypes releases the GIL)."""
+    import threading
     from heligym_amd import config
     from oracle.oracle import Oracle
     cfg, doc = config.make_config(task=task, dt=dt)
@@ -80,13 +82,32 @@ def cpu_baseline(dt, task, seconds):
     t0 = time.perf_counter()
     n0, _ = orc.rollout(tr, 1, 2000, seed=1)
     rate0 = n0 / (time.perf_counter() - t0)
-    steps = max(1000, int(rate0 * seconds / 64))
+    single_s = seconds * 0.6
+    steps = max(1000, int(rate0 * single_s / 64))
     t0 = time.perf_counter()
     n, _ = orc.rollout(tr, 64, steps, seed=2)
     el = time.perf_counter() - t0
-    return {"value": n / el, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"oracle/heli_oracle.c, 64 envs x {steps} steps (dt={dt}, U(-1,1) actions, "
-                      f"turbulence on, auto-reset), {el:.1f} s on 1 host core"}
+    single = n / el
+    threads = max(1, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    wall = seconds * 0.4 / max(1, threads // 4)   # bounded CPU work: ~0.4 x seconds x 4 core-seconds
+    per = max(500, int(rate0 * wall / 16))        # steps per thread (16 envs each) for ~`wall` s
+    done = [0] * threads
+
+    def work(k):
+        done[k] = orc.rollout(tr, 16, per, seed=100 + k)[0]
+
+    ts = [threading.Thread(target=work, args=(k,)) for k in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    elm = time.perf_counter() - t0
+    return {"value": sum(done) / elm, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "single_core_value": single,
+            "sample": f"oracle/heli_oracle.c (dt={dt}, U(-1,1) actions, turbulence on, auto-reset): "
+                      f"{threads} threads x 16 envs x {per} steps in {elm:.1f} s; single core 64 envs x "
+                      f"{steps} steps in {el:.1f} s"}
 
 
 def parity_error(dt, task):
