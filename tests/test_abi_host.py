@@ -135,3 +135,33 @@ def test_reset_mode_is_validated(lib, terrain_u16):
     h = ctypes.c_void_p()
     assert lib.hg_create(ctypes.byref(bad), hm.ctypes.data, 1024, 1024, 16, ctypes.byref(h)) == -1
     assert b"reset_mode" in lib.hg_last_error()
+
+
+def _build_c_example(tmp_path):
+    exe = tmp_path / "c_abi_step"
+    cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-I",
+           "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__", os.path.join(ROOT, "examples", "c_abi_step.c"),
+           "-L", os.path.dirname(_abi.LIB_PATH), "-lheligym_amd", "-L", "/opt/rocm/lib", "-lamdhip64",
+           "-o", str(exe)]
+    import subprocess
+    subprocess.check_call(cmd)
+    return exe
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/include/hip/hip_runtime_api.h"), reason="no ROCm headers")
+def test_plain_c_host_compiles_against_header(tmp_path):
+    """The C-ABI is usable from plain C (gcc, no torch): examples/c_abi_step.c builds and links."""
+    assert _build_c_example(tmp_path).exists()
+
+
+@pytest.mark.gpu
+def test_plain_c_host_runs(tmp_path):
+    import subprocess
+    exe = _build_c_example(tmp_path)
+    env = dict(os.environ, LD_LIBRARY_PATH=os.path.dirname(_abi.LIB_PATH) + ":/opt/rocm/lib")
+    out = subprocess.run([str(exe), "4096", "200"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    f = dict(zip(out.stdout.split()[0::2], out.stdout.split()[1::2]))
+    assert int(f["envs"]) == 4096 and int(f["resets"]) == 0
+    assert abs(float(f["mean_ground_alt_ft"]) - (100 + 38.5 / 12)) < 5.0    # trimmed hover holds altitude
+    assert 400 < float(f["mean_power_hp"]) < 800
