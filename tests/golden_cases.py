@@ -159,3 +159,18 @@ def f8_resets():
 def f8_episodes():
     d = np.load(os.path.join(GOLDEN, "reset_f8.npz"), allow_pickle=False)
     return {k.split("/", 1)[1]: d[k] for k in d.files if k.startswith("episode/")}
+
+
+VARIANTS = ("turb5", "turb7_wind", "turb0", "heavy")
+
+
+def load_variant(name):
+    """traj_var_<name>.npz and the airframe document it was recorded with: the bundled AW109
+    parameters with the recorded edits applied (turbulence level, mean wind, mass, rotor speeds)."""
+    import copy
+    import json
+    from heligym_amd import config
+    d = np.load(os.path.join(GOLDEN, f"traj_var_{name}.npz"), allow_pickle=False)
+    doc = copy.deepcopy(config.load_airframe("aw109"))
+    doc["airframe"].update(json.loads(str(d["airframe_edits_json"])))
+    return d, doc

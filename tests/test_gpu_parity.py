@@ -28,8 +28,8 @@ def make_env(torch, n, task, dt, autoreset=False, **kw):
                       target={"vel": 100.0, "heading": 0.0} if task == "forward_flight" else None, **kw)
 
 
-def run_single_steps(torch, batch, task):
-    env = make_env(torch, len(batch["state"]), task, batch["dt"])
+def run_single_steps(torch, batch, task, **env_kw):
+    env = make_env(torch, len(batch["state"]), task, batch["dt"], **env_kw)
     env.set_state(batch["state"].astype(np.float32), batch["counters"].astype(np.int32))
     act = torch.as_tensor(batch["actions"].astype(np.float32), device=env.device)
     eta = torch.as_tensor(batch["eta"].astype(np.float32), device=env.device)
@@ -50,13 +50,28 @@ def run_single_steps(torch, batch, task):
 def test_single_step_vs_reference(torch, tag, task):
     b = gc.single_step_batch(gc.load(tag), task)
     out = run_single_steps(torch, b, task)
+    check_vs_reference(b, out, task, f"{task} dt={tag}")
+
+
+@pytest.mark.parametrize("name", gc.VARIANTS)
+def test_single_step_vs_reference_parameter_variants(torch, name):
+    """Turbulence levels 0 / 5 / 7, another mean wind, a heavier airframe with other rotor speeds:
+    the kernel against the reference's steps recorded with those parameters (generic loader)."""
+    d, doc = gc.load_variant(name)
+    b = gc.single_step_batch(d, "hover")
+    out = run_single_steps(torch, b, "hover", heli_name=doc)
+    check_vs_reference(b, out, "hover", f"variant {name}")
+
+
+def check_vs_reference(b, out, task, label):
+    tag = label
     e_obs = gc.step_errors(out["obs"], b["obs"], gc.OBS_ANGLE_COLS)
     e_heli = gc.step_errors(out["state"][:, :18], b["heli"], gc.HELI_ANGLE_COLS)
     e_wind = gc.step_errors(out["state"][:, 18:23], b["wind"])
     tol_obs = STEP_ABS + STEP_REL * np.abs(b["obs"])
     tol_heli = STEP_ABS + STEP_REL * np.abs(b["heli"])
     tol_wind = STEP_ABS + STEP_REL * np.abs(b["wind"])
-    print(f"\n[{task} dt={tag}] {len(b['obs'])} steps: max|d obs| {e_obs.max():.3e}  "
+    print(f"\n[{tag}] {len(b['obs'])} steps: max|d obs| {e_obs.max():.3e}  "
           f"max|d state| {e_heli.max():.3e}  max|d wind| {e_wind.max():.3e}  "
           f"max|d reward| {np.abs(out['reward'] - b['reward']).max():.3e}")
     # The golden pre-step states are fp64; the kernel receives them rounded to fp32.  In ground

@@ -16,6 +16,10 @@ trim.npz         Newton trim results (helicopter_dynamics.py:491-576) for severa
 traj_dt0.02.npz  per-step trajectories of `Heli.step` (helicopter.py:192-206) for
 traj_dt0.01.npz  scenarios covering every branch of the step (see SCENARIOS), with the
                  recorded turbulence noise `eta` so the step can be replayed exactly.
+traj_var_<v>.npz trajectories like traj_dt*.npz for modified parameter documents (turbulence
+                 levels 0/5/7, another mean wind, a heavier airframe with other rotor speeds), with
+                 the parameter edits (JSON, flat airframe keys) so tests rebuild the same
+                 configuration.
 reset_f8.npz     second-episode resets (F8): the reference re-trims against the wind of the
                  last step (helicopter.py:198, helicopter_dynamics.py:66-71,491-555) -- winds,
                  reset states for several trim conditions / dt, and terminal steps of episodes
@@ -221,6 +225,64 @@ def _action(kind, trim_a, arng):
     raise ValueError(kind)
 
 
+VARIANTS = {   # name -> (dt, edits of the reference yaml, scenarios (name, trim, action kind, steps))
+    "turb5": (0.01, {("ENV", "TURB_LVL"): 5},
+              [("hover", {}, "trim_noise", 150), ("alt1500", {"gr_alt": 1500.0}, "trim_noise", 150),
+               ("alt2500", {"gr_alt": 2500.0}, "trim_noise", 150)]),
+    "turb7_wind": (0.02, {("ENV", "TURB_LVL"): 7, ("ENV", "WIND_SPD"): 35.0, ("ENV", "WIND_DIR"): 120.0},
+                   [("hover", {}, "trim_noise", 150), ("alt2500_fwd", {"gr_alt": 2500.0, "ned_vel": [60.0, 0.0, 0.0]},
+                                                    "trim_noise", 150), ("random", {}, "uniform", 200)]),
+    "turb0": (0.02, {("ENV", "TURB_LVL"): 0}, [("hover", {}, "trim_noise", 120), ("alt2500", {"gr_alt": 2500.0},
+                                                                                 "trim_noise", 120)]),
+    "heavy": (0.01, {("HELI", "WT"): 6200.0, ("HELI", "IX"): 1800.0, ("HELI", "MR", "RPM"): 400.0,
+                     ("HELI", "TR", "RPM"): 2150.0, ("HELI", "FS_CG"): 134.0},
+              [("hover", {}, "trim_noise", 150), ("fwd80", {"ned_vel": [80.0, 0.0, 0.0]}, "trim_noise", 150),
+               ("crash", {}, "low_collective", 300)]),
+}
+
+
+def gen_variant(ns, name):
+    import copy
+    import tempfile
+    import yaml
+    dt, edits, scen = VARIANTS[name]
+    with open(os.path.join(refload.ENVS_DIR, "helis", "aw109.yaml")) as f:
+        doc = yaml.safe_load(f)
+    doc = copy.deepcopy(doc)
+    for path, v in edits.items():
+        node = doc
+        for k in path[:-1]:
+            node = node[k]
+        node[path[-1]] = v
+    tmp = tempfile.NamedTemporaryFile("w", suffix=".yaml", delete=False)
+    yaml.safe_dump(doc, tmp)
+    tmp.close()
+    heli_name = tmp.name[:-5]   # Heli() appends ".yaml"; os.path.join keeps an absolute path
+    # record only the edits, in this package's flat airframe keys (tests apply them to the bundled
+    # AW109 document through the generic loader)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "heli-gym_amd"))
+    from heligym_amd import config as hg_config
+    flat = {}
+    for path, v in edits.items():
+        if path[0] == "ENV":
+            flat[hg_config._REF_ENV_KEYS[path[1]]] = v
+        elif len(path) == 3:
+            flat[hg_config._REF_SECTIONS[path[1]] + path[2]] = v
+        else:
+            flat[path[1]] = v
+    out = {"airframe_edits_json": np.array(json.dumps(flat)), "dt": np.array(dt)}
+    names = []
+    ns.helicopter.DT = dt
+    for i, (sname, cond, kind, steps) in enumerate(scen):
+        env = ns.tasks.HeliHover(heli_name)
+        env.set_target({"vel": 100, "heading": 0})
+        out.update(run_scenario(ns, dt, sname, cond, kind, steps, seed=300 + i, env=env))
+        names.append(sname)
+    out["scenarios"] = np.array(names)
+    os.unlink(tmp.name)
+    return out
+
+
 def gen_f8(ns):
     out = {}
     rows = {k: [] for k in ["dt", "cond", "wind_ned", "state", "action", "obs"]}
@@ -281,8 +343,8 @@ def gen_f8(ns):
     return out
 
 
-def run_scenario(ns, dt, name, cond, kind, max_steps, seed):
-    env = make_env(ns, dt)
+def run_scenario(ns, dt, name, cond, kind, max_steps, seed, env=None):
+    env = make_env(ns, dt) if env is None else env
     env.set_trim_cond(cond)
     np.random.seed(seed)                    # turbulence noise (wind_dynamics.py:52, global RNG)
     arng = np.random.RandomState(seed + 1000)  # actions
@@ -347,6 +409,10 @@ def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     if only in (None, "f8"):
         np.savez_compressed(os.path.join(OUT, "reset_f8.npz"), **gen_f8(ns))
+    if only in (None, "variants"):
+        for v in VARIANTS:
+            np.savez_compressed(os.path.join(OUT, f"traj_var_{v}.npz"), **gen_variant(ns, v))
+            print("variant", v, flush=True)
     if only is not None:
         return
     meta = {"numpy": np.__version__, "generator": "tools/gen_goldens.py",
