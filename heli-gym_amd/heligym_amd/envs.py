@@ -8,7 +8,7 @@ window) is not part of this package: render() raises NotImplementedError.
 """
 import numpy as np
 
-from . import config
+from . import _abi, config
 from .vector import HeliVecEnv
 
 
@@ -29,7 +29,14 @@ class Heli:
         self.max_time = self._env.max_time
         self.success_duration = self.max_time / 4
         self.task_duration = self.max_time / 4
-        self._act = self._env.torch.zeros((1, 4), dtype=self._env.torch.float32, device=self._env.device)
+        t = self._env.torch
+        self._act = t.zeros((1, 4), dtype=t.float32, device=self._env.device)
+        # pinned host staging: one async H2D copy of the action, async D2H copies of the results
+        # and a single stream synchronisation per step
+        self._h_act = t.zeros((1, 4), dtype=t.float32).pin_memory()
+        self._h_obs = t.zeros((1, 17), dtype=t.float32).pin_memory()
+        self._h_rew = t.zeros((1,), dtype=t.float32).pin_memory()
+        self._h_flags = t.zeros((3,), dtype=t.uint8).pin_memory()
 
     # setters (helicopter.py:89-111)
     def set_max_time(self, max_time=None):
@@ -63,10 +70,21 @@ class Heli:
 
     def step(self, actions):
         """helicopter.py:192-206 -> (obs, reward, terminated, truncated, info)."""
-        self._act.copy_(self._env.torch.as_tensor(np.asarray(actions, dtype=np.float32).reshape(1, 4)))
-        obs, rew, term, trunc, info = self._env.step(self._act)
-        info = {k: bool(info[k][0]) for k in ("failed", "successed", "time_up")}
-        return obs[0].cpu().numpy().copy(), float(rew[0]), bool(term[0]), bool(trunc[0]), info
+        e = self._env
+        self._h_act.numpy()[0] = np.asarray(actions, dtype=np.float32).reshape(4)
+        self._act.copy_(self._h_act, non_blocking=True)
+        e.step_async(self._act, with_reset_info=False)
+        self._h_obs.copy_(e.obs, non_blocking=True)
+        self._h_rew.copy_(e.reward, non_blocking=True)
+        self._h_flags[0:1].copy_(e.terminated_u8, non_blocking=True)
+        self._h_flags[1:2].copy_(e.truncated_u8, non_blocking=True)
+        self._h_flags[2:3].copy_(e.info_u8, non_blocking=True)
+        e.torch.cuda.current_stream(e.device).synchronize()
+        fl = self._h_flags.numpy()
+        bits = int(fl[2])
+        info = {"failed": bool(bits & _abi.HG_INFO_FAILED), "successed": bool(bits & _abi.HG_INFO_SUCCESSED),
+                "time_up": bool(bits & _abi.HG_INFO_TIME_UP)}
+        return self._h_obs.numpy()[0].copy(), float(self._h_rew.numpy()[0]), bool(fl[0]), bool(fl[1]), info
 
     def render(self):
         raise NotImplementedError("rendering is outside heligym_amd (the reference renders with OpenGL)")

@@ -290,6 +290,21 @@ def test_single_env_dropin(torch):
     np.testing.assert_allclose(obs, t["hover_zero/init_obs"], rtol=1e-4, atol=1e-3)
     obs, r, term, trunc, info = env.step(np.zeros(4, np.float32))
     assert isinstance(r, float) and isinstance(term, bool) and isinstance(trunc, bool)
+    # BASELINE config 1: 10 000 zero-action steps with a reset on every termination;
+    # the reference records 15 resets (episodes end by a crash after ~643 steps)
+    env.reset()
+    resets, lengths, t = 0, [], 0
+    for _ in range(10000):
+        obs, r, term, trunc, info = env.step(np.zeros(4, np.float32))
+        t += 1
+        if term or trunc:
+            assert info["failed"] and not trunc
+            env.reset()
+            resets += 1
+            lengths.append(t)
+            t = 0
+    assert 14 <= resets <= 16, resets
+    assert 600 <= np.median(lengths) <= 690, lengths
     env.close()
 
 
