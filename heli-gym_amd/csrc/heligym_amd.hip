@@ -23,6 +23,7 @@
 #include "../../include/heligym_amd.h"
 #include "physics.h"
 #include "trim.h"
+#include "retrim.h"
 
 using hg::Params;
 using hg::Template;
@@ -92,6 +93,7 @@ struct StepArgs {
     float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
     int32_t* retrim_list;    // ... compacted ids of the envs to re-trim
     int32_t* retrim_count;   // ... their number (zeroed before the launch)
+    const float* tmpl_env;   // per-env reset templates [N][39] (Params::env_templates), else unused
     int32_t nsteps;          // MULTI: steps per launch (inputs / outputs stacked [nsteps][N])
     int64_t n;
     uint64_t seed;
@@ -368,16 +370,28 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
             if (do_reset) a.retrim_list[base + __popcll(mask & ((1ull << lane) - 1ull))] = (int32_t)i;
         }
     }
-    if (do_reset) {
+    if (FEAT && P.env_templates) {   // this env's own reset target (its own trim condition)
+        if (do_reset) {
+            const float* tr = a.tmpl_env + (int64_t)i * kTplFloats;
+#pragma unroll
+            for (int c = 0; c < 18; ++c) hs[c] = tr[c];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) carry[c] = tr[18 + c];
+#pragma unroll
+            for (int c = 0; c < 17; ++c) obs[c] = tr[22 + c];
+        }
+    } else if (do_reset) {
         // Template<float> = heli[18] | carry[4] | obs[17], float c held by lane c
 #pragma unroll
         for (int c = 0; c < 18; ++c) hs[c] = lane_value(tpl, c);
 #pragma unroll
-        for (int c = 0; c < 5; ++c) ws[c] = 0.f;
-#pragma unroll
         for (int c = 0; c < 4; ++c) carry[c] = lane_value(tpl, 18 + c);
 #pragma unroll
         for (int c = 0; c < 17; ++c) obs[c] = lane_value(tpl, 22 + c);
+    }
+    if (do_reset) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) ws[c] = 0.f;
         step = 0;
         succ = 0;
         epi += 1;
@@ -414,195 +428,6 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
 #endif
 }
 
-// ------------------------------------------------------------------------------ device re-trim
-// HelicopterDynamics.trim (helicopter_dynamics.py:491-555) for many winds at once: the reset path of
-// reset_mode RETRIM (F8) and hg_trim_batch.  One wave per trim, fp64 throughout, every lane holding
-// the same Newton iterate:
-//   * lanes 0..15 / 16..31 evaluate the +eps / -eps Jacobian columns in parallel;
-//   * lane j <= 16 then holds column j of [J | r] in registers and the Gauss-Jordan elimination
-//     (hg::solve16, same operation order) runs with the pivot column broadcast by readlane;
-//   * lanes 0..9 evaluate the ten step-halving trials at once; the first one that lowers the
-//     residual is the trial the reference's sequential search accepts.
-struct RetrimArgs {
-    const Params<double>* P;
-    const hg::TrimSetup* T;
-    const int32_t* count;   // env mode: device job count; batch mode: NULL (count = njobs)
-    int64_t njobs;
-    const int32_t* list;    // env mode: env id of each job
-    const float* wind;      // [N,3] by env id (env mode) or [count,3] by job (batch mode)
-    float* state;           // env mode: SoA state (heli 18 and carry 4 rewritten)
-    float* obs;             // env mode: [N,17] reset observation rows, or NULL
-    int64_t n;
-    float* out_state;       // batch mode outputs (rows by job), each may be NULL
-    float* out_action;
-    float* out_obs;
-    int32_t* out_status;
-    int32_t* fail_count;    // env mode: trims that failed (env keeps the template reset)
-};
-
-__device__ __forceinline__ double read_lane(double v, int lane) {
-    const uint64_t u = __double_as_longlong(v);
-    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, lane);
-    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-__device__ __forceinline__ double shfl_d(double v, int src) {
-    const uint64_t u = __double_as_longlong(v);
-    const uint32_t lo = __shfl((int)(uint32_t)u, src);
-    const uint32_t hi = __shfl((int)(uint32_t)(u >> 32), src);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-__device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, int64_t env, const double x[16],
-                                             const double s[18], const double ob[17]) {
-    if (a.list) {
-        for (int c = 0; c < 18; ++c) a.state[(int64_t)c * a.n + env] = (float)s[c];
-        const int co[4] = {4, 5, 6, 16};
-        for (int c = 0; c < 4; ++c) a.state[(int64_t)(23 + c) * a.n + env] = (float)ob[co[c]];
-        if (a.obs)
-            for (int c = 0; c < 17; ++c) a.obs[env * 17 + c] = (float)ob[c];
-    } else {
-        if (a.out_state)
-            for (int c = 0; c < 18; ++c) a.out_state[job * 18 + c] = (float)s[c];
-        if (a.out_action)
-            for (int c = 0; c < 4; ++c) a.out_action[job * 4 + c] = (float)x[12 + c];
-        if (a.out_obs)
-            for (int c = 0; c < 17; ++c) a.out_obs[job * 17 + c] = (float)ob[c];
-    }
-    if (a.out_status) a.out_status[job] = HG_OK;
-}
-
-// Lane roles per evaluation round: lanes 0..31 the Jacobian columns at the point the next Newton
-// step will start from, lanes 32..41 the ten step-halving trials of the current step (trial 0,
-// the full step, is that point whenever the search accepts it, which it usually does), lane 32
-// alone the residual at x0 in the first round.  A round is one trim_fcn latency; a trim of three
-// Newton steps takes four rounds.
-__global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
-    const int l = threadIdx.x;
-    const Params<double>& P = *a.P;
-    const hg::TrimSetup& T = *a.T;
-    const double eps = hg::kTrimEps;
-    const int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
-    for (int64_t job = blockIdx.x; job < jobs; job += gridDim.x) {   // uniform per wave
-        const int64_t env = a.list ? (int64_t)a.list[job] : job;
-        const float* wr = a.wind + 3 * (a.list ? env : job);
-        const double W[3] = {(double)wr[0], (double)wr[1], (double)wr[2]};
-        double x[16], y[16], dir[16];
-        for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; }
-        double tol = 0;
-        int it = 0;
-        bool ok = true, done = false, first = true, have_jac = false;
-        while (!done) {
-            // ---- one evaluation round
-            const int c = l & 15;
-            const int j = l - 32;   // line-search trial of this lane (0..9), first round: base point
-            double xe[16];
-            if (l < 32) {   // Jacobian columns at x - dir (= x in the first round)
-                for (int k = 0; k < 16; ++k) {
-                    const double xs = first ? x[k] : x[k] - 1.0 * dir[k];
-                    xe[k] = k == c ? (l < 16 ? xs + eps : xs - eps) : xs;
-                }
-            } else {
-                const double step = (j >= 0 && j < hg::kTrimLineSearch) ? ldexp(1.0, -j) : 0.0;
-                for (int k = 0; k < 16; ++k) xe[k] = first ? x[k] : x[k] - step * dir[k];
-            }
-            double ye[16], se[18], de[18], oe[17];
-            hg::trim_fcn(P, T.base, xe, W, T.hc, ye, se, de, oe);
-            const double te = hg::trim_residual(ye, T.yt);
-            // ---- accept a trial (or take the base point)
-            int src = 32;   // lane whose evaluation is the new iterate
-            if (first) {
-                first = false;
-                have_jac = true;
-            } else {
-                int js = hg::kTrimLineSearch;
-                for (int jj = hg::kTrimLineSearch - 1; jj >= 0; --jj)
-                    if (read_lane(te, 32 + jj) < tol) js = jj;
-                if (js >= hg::kTrimLineSearch - 1) {   // helicopter_dynamics.py:540: keep x
-                    done = true;
-                    src = -1;
-                } else {
-                    const double step = ldexp(1.0, -js);
-                    for (int k = 0; k < 16; ++k) x[k] = x[k] - step * dir[k];
-                    src = 32 + js;
-                    have_jac = js == 0;   // the Jacobian lanes evaluated around trial 0
-                    if (++it > hg::kTrimMaxIter) { ok = false; done = true; src = -1; }
-                }
-            }
-            if (src >= 0) {
-                for (int k = 0; k < 16; ++k) y[k] = read_lane(ye[k], src);
-                tol = read_lane(te, src);
-                if (!(tol > eps)) {   // converged: the accepting lane holds the final evaluation
-                    done = true;
-                    if (l == src) retrim_write(a, job, env, x, se, oe);
-                    break;
-                }
-            }
-            if (done) break;
-            if (!have_jac) {   // the search accepted a shorter step: Jacobian at the new x
-                if (l < 32) {
-                    for (int k = 0; k < 16; ++k) xe[k] = k == c ? (l < 16 ? x[k] + eps : x[k] - eps) : x[k];
-                    hg::trim_fcn(P, T.base, xe, W, T.hc, ye, nullptr, nullptr, nullptr);
-                }
-            }
-            // ---- Newton direction: Gauss-Jordan (hg::solve16), lane j <= 16 owns column j of [J | r]
-            double col[16];
-            for (int k = 0; k < 16; ++k) {
-                const double ym = shfl_d(ye[k], (l + 16) & 63);
-                col[k] = l < 16 ? (ye[k] - ym) / (2 * eps) : y[k] - T.yt[k];
-            }
-#pragma unroll
-            for (int cc = 0; cc < 16; ++cc) {
-                double bc[16];   // column cc, broadcast to every lane
-#pragma unroll
-                for (int k = 0; k < 16; ++k) bc[k] = read_lane(col[k], cc);
-                int p = cc;
-#pragma unroll
-                for (int i = cc + 1; i < 16; ++i)
-                    if (fabs(bc[i]) > fabs(bc[p])) p = i;
-                p = __builtin_amdgcn_readfirstlane(p);
-                double mp = bc[cc];
-#pragma unroll
-                for (int i = cc + 1; i < 16; ++i)
-                    if (i == p) mp = bc[i];
-                if (mp == 0.0 || !isfinite(mp)) { ok = false; break; }
-                if (p != cc) {
-#pragma unroll
-                    for (int i = cc + 1; i < 16; ++i)
-                        if (i == p) {
-                            double t = col[cc]; col[cc] = col[i]; col[i] = t;
-                            t = bc[cc]; bc[cc] = bc[i]; bc[i] = t;
-                        }
-                }
-                const double piv = bc[cc];
-                if (l >= cc) col[cc] /= piv;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    if (i == cc) continue;
-                    const double f = bc[i];
-                    if (l >= cc && f != 0.0) col[i] -= f * col[cc];
-                }
-            }
-            if (!ok) break;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) dir[k] = read_lane(col[k], 16);
-        }
-        if (ok && done && l == 0) {
-            // the search stopped without converging (:540): final evaluation at the kept x
-            bool written = !(tol > eps);
-            if (!written) {
-                double yy[16], s[18], d[18], ob[17];
-                hg::trim_fcn(P, T.base, x, W, T.hc, yy, s, d, ob);
-                retrim_write(a, job, env, x, s, ob);
-            }
-        }
-        if (!ok && l == 0) {
-            if (a.fail_count) atomicAdd(a.fail_count, 1);
-            if (a.out_status) a.out_status[job] = HG_E_TRIM;
-        }
-    }
-}
-
 // reset_mode RETRIM bookkeeping: the wind each env's next reset is trimmed against (the mean wind
 // until the env has stepped, helicopter.py:55), and the compacted list of masked envs of hg_reset.
 __global__ __launch_bounds__(kBlock) void fill_wind_kernel(float* wind, int64_t n, float w0, float w1, float w2) {
@@ -627,23 +452,25 @@ __global__ __launch_bounds__(kBlock) void mask_list_kernel(const uint8_t* mask, 
 }
 
 // Heli.reset for masked envs (helicopter.py:208-217)
-__global__ __launch_bounds__(kBlock) void reset_kernel(const Template<float> T, float* state, int32_t* counters,
-                                                       const uint8_t* mask, float* obs, int64_t n) {
+__global__ __launch_bounds__(kBlock) void reset_kernel(const Template<float> T, const float* tmpl_env, float* state,
+                                                       int32_t* counters, const uint8_t* mask, float* obs, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     if (mask && !mask[i]) return;
+    // the shared template, or this env's own ([N][39] = heli 18 | carry 4 | obs 17)
+    const float* tr = tmpl_env ? tmpl_env + i * kTplFloats : reinterpret_cast<const float*>(&T);
 #pragma unroll
-    for (int c = 0; c < 18; ++c) state[c * n + i] = T.heli[c];
+    for (int c = 0; c < 18; ++c) state[c * n + i] = tr[c];
 #pragma unroll
     for (int c = 0; c < 5; ++c) state[(18 + c) * n + i] = 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) state[(23 + c) * n + i] = T.carry[c];
+    for (int c = 0; c < 4; ++c) state[(23 + c) * n + i] = tr[18 + c];
     counters[i] = 0;
     counters[n + i] = 0;
     counters[2 * n + i] += 1;
     if (obs) {
 #pragma unroll
-        for (int c = 0; c < 17; ++c) obs[i * 17 + c] = T.obs[c];
+        for (int c = 0; c < 17; ++c) obs[i * 17 + c] = tr[22 + c];
     }
 }
 
@@ -952,7 +779,18 @@ struct hg_env {
     float* retrim_wind = nullptr;           // reset_mode RETRIM work buffers
     int32_t* retrim_list = nullptr;
     int32_t* retrim_count = nullptr;        // [0] jobs of the current step, [1] failures so far
+    float* tmpl_env = nullptr;              // per-env reset templates [N][39] (hg_set_reset_templates)
+    bool env_templates = false;
+    hg::TrimSetup* setup_batch = nullptr;   // hg_trim_conds_batch scratch
+    int64_t setup_batch_cap = 0;
 };
+
+// Model constants after a configuration change (create and the setters).
+static void rederive(hg_env* e) {
+    e->Pd = derive<double>(e->cfg, e->rows, e->cols);
+    e->Pf = derive<float>(e->cfg, e->rows, e->cols);
+    e->Pf.env_templates = e->env_templates ? 1 : 0;
+}
 
 // Upload the fp32 model constants the step kernel reads (after create and every setter).
 static int32_t upload_params(hg_env* e) {
@@ -1079,6 +917,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     auto cleanup = [&](hipError_t err, const char* what) {
         dfree(e->hmap); dfree(e->state); dfree(e->counters); dfree(e->tmpl_dev); dfree(e->params_dev);
         dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_count);
+        dfree(e->tmpl_env); dfree(e->setup_batch);
         delete e;
         return fail(HG_E_HIP, std::string(what) + ": " + hipGetErrorString(err));
     };
@@ -1135,6 +974,8 @@ void hg_destroy(hg_env* e) {
     dfree(e->retrim_wind);
     dfree(e->retrim_list);
     dfree(e->retrim_count);
+    dfree(e->tmpl_env);
+    dfree(e->setup_batch);
     delete e;
 }
 
@@ -1143,16 +984,14 @@ int64_t hg_num_envs(const hg_env* e) { return e ? e->n : -1; }
 int32_t hg_set_max_time(hg_env* e, double max_time) {
     if (!e || !(max_time > 0)) return fail(HG_E_INVALID, "bad env or max_time");
     e->cfg.max_time = max_time;
-    e->Pd = derive<double>(e->cfg, e->rows, e->cols);
-    e->Pf = derive<float>(e->cfg, e->rows, e->cols);
+    rederive(e);
     return upload_params(e);
 }
 
 int32_t hg_set_target(hg_env* e, const hg_target* t) {
     if (!e || !t) return fail(HG_E_INVALID, "bad env or target");
     e->cfg.target = *t;
-    e->Pd = derive<double>(e->cfg, e->rows, e->cols);
-    e->Pf = derive<float>(e->cfg, e->rows, e->cols);
+    rederive(e);
     return upload_params(e);
 }
 
@@ -1175,13 +1014,13 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(reset_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->tmpl,
-                       e->state, e->counters, mask, obs, e->n);
+                       e->Pf.env_templates ? e->tmpl_env : nullptr, e->state, e->counters, mask, obs, e->n);
     HIP_TRY(hipGetLastError());
     if (e->cfg.reset_mode == HG_RESET_RETRIM) {   // trim each masked env against its last wind (F8)
         HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
         hipLaunchKernelGGL(mask_list_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, mask, e->n, e->retrim_list,
                            e->retrim_count);
-        RetrimArgs r;
+        hgk::RetrimArgs r;
         memset(&r, 0, sizeof(r));
         r.P = e->pd_dev;
         r.T = e->setup_dev;
@@ -1192,7 +1031,7 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
         r.obs = obs;
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
-        hipLaunchKernelGGL(retrim_kernel, dim3(retrim_grid(e->n)), dim3(64), 0, s, r);
+        HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), s));
         HIP_TRY(hipGetLastError());
     }
     return HG_OK;
@@ -1229,12 +1068,14 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     a.retrim_wind = e->retrim_wind;
     a.retrim_list = e->retrim_list;
     a.retrim_count = e->retrim_count;
+    a.tmpl_env = e->tmpl_env;
     a.nsteps = 1;
     a.n = e->n;
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;
     const dim3 grid(grid_for(e->n)), block(kBlock);
-    const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX;
+    const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next ||
+                      e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
 #define HG_LAUNCH_STEP_NT(T, NT)                                                                                 \
     do {                                                                                                         \
         if (feat) {                                                                                              \
@@ -1258,7 +1099,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
 #undef HG_LAUNCH_STEP_NT
     HIP_TRY(hipGetLastError());
     if (retrim) {   // re-trim this step's resets against their last wind (overwrites the template)
-        RetrimArgs r;
+        hgk::RetrimArgs r;
         memset(&r, 0, sizeof(r));
         r.P = e->pd_dev;
         r.T = e->setup_dev;
@@ -1269,7 +1110,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
         r.obs = obs;
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
-        hipLaunchKernelGGL(retrim_kernel, dim3(retrim_grid(e->n)), dim3(64), 0, s, r);
+        HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), s));
     }
 #undef HG_LAUNCH_STEP
     HIP_TRY(hipGetLastError());
@@ -1298,13 +1139,14 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     a.truncated = truncated;
     a.info = info;
     a.eta = eta;
+    a.tmpl_env = e->tmpl_env;
     a.nsteps = nsteps;
     a.n = e->n;
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid(grid_for(e->n)), block(kBlock);
-    const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX;
+    const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
 #define HG_LAUNCH_ROLL_NT(T, NT)                                                                                 \
     do {                                                                                                         \
         if (feat) {                                                                                              \
@@ -1336,7 +1178,7 @@ int32_t hg_trim_batch(hg_env* e, const float* wind, int64_t count, float* state,
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     if (count < 0 || (count > 0 && !wind)) return fail(HG_E_INVALID, "bad wind / count");
     if (count == 0) return HG_OK;
-    RetrimArgs r;
+    hgk::RetrimArgs r;
     memset(&r, 0, sizeof(r));
     r.P = e->pd_dev;
     r.T = e->setup_dev;
@@ -1346,9 +1188,57 @@ int32_t hg_trim_batch(hg_env* e, const float* wind, int64_t count, float* state,
     r.out_action = action;
     r.out_obs = obs;
     r.out_status = status;
-    hipLaunchKernelGGL(retrim_kernel, dim3(retrim_grid(count)), dim3(64), 0, (hipStream_t)stream, r);
+    HIP_TRY(hgk::launch_retrim(r, retrim_grid(count), (hipStream_t)stream));
     HIP_TRY(hipGetLastError());
     return HG_OK;
+}
+
+int32_t hg_trim_conds_batch(hg_env* e, const hg_trim_cond* conds, int64_t count, const float* wind, float* state,
+                            float* action, float* obs, int32_t* status, void* stream) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    if (count < 0 || (count > 0 && !conds)) return fail(HG_E_INVALID, "bad conds / count");
+    if (count == 0) return HG_OK;
+    if (count > e->setup_batch_cap) {
+        dfree(e->setup_batch);
+        e->setup_batch = nullptr;
+        e->setup_batch_cap = 0;
+        HIP_TRY(hipMalloc(&e->setup_batch, sizeof(hg::TrimSetup) * count));
+        e->setup_batch_cap = count;
+    }
+    std::vector<hg::TrimSetup> host((size_t)count);
+    for (int64_t j = 0; j < count; ++j) host[j] = trim_setup(e->Pd, e->hmap_host.data(), conds[j]);
+    hipStream_t s = (hipStream_t)stream;
+    HIP_TRY(hipMemcpyAsync(e->setup_batch, host.data(), sizeof(hg::TrimSetup) * count, hipMemcpyHostToDevice, s));
+    hgk::RetrimArgs r;
+    memset(&r, 0, sizeof(r));
+    r.P = e->pd_dev;
+    r.T = e->setup_batch;
+    r.setup_stride = 1;
+    r.njobs = count;
+    r.wind = wind;
+    r.out_state = state;
+    r.out_action = action;
+    r.out_obs = obs;
+    r.out_status = status;
+    HIP_TRY(hgk::launch_retrim(r, retrim_grid(count), s));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(s));   // the host staging of the setups is released on return
+    return HG_OK;
+}
+
+int32_t hg_set_reset_templates(hg_env* e, const float* templates, void* stream) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    if (templates && e->cfg.reset_mode == HG_RESET_RETRIM)
+        return fail(HG_E_INVALID, "per-env reset templates need reset_mode HG_RESET_TEMPLATE");
+    if (templates) {
+        if (!e->tmpl_env) HIP_TRY(hipMalloc(&e->tmpl_env, sizeof(float) * kTplFloats * e->n));
+        HIP_TRY(hipMemcpyAsync(e->tmpl_env, templates, sizeof(float) * kTplFloats * e->n, hipMemcpyDeviceToDevice,
+                               (hipStream_t)stream));
+        HIP_TRY(hipStreamSynchronize((hipStream_t)stream));
+    }
+    e->env_templates = templates != nullptr;
+    e->Pf.env_templates = e->env_templates ? 1 : 0;
+    return upload_params(e);
 }
 
 int32_t hg_retrim_failures(hg_env* e, int64_t* count) {

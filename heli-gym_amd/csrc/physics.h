@@ -163,6 +163,7 @@ struct Params {
     R fail_zdot, fail_ang;
     int32_t task, time_up_steps, success_steps, autoreset, reset_retrim;
     int32_t autoreset_next, max_episode_steps;   // next-step auto-reset; TimeLimit (INT32_MAX: off)
+    int32_t env_templates;                       // per-env reset templates set (hg_set_reset_templates)
 };
 
 // Reset template: trimmed heli state, zero turbulence state, carry and observation.

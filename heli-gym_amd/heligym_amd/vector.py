@@ -294,6 +294,46 @@ class HeliVecEnv:
         self._keep_trim = w
         return out
 
+    def trim_conds(self, conds, wind_ned=None):
+        """Device trims (hg_trim_conds_batch) for a list of trim-condition dicts (the reference's
+        set_trim_cond keys, missing keys from the defaults), against `wind_ned` [K,3] or the mean
+        wind.  Returns dict of device tensors state [K,18], action [K,4], obs [K,17], status [K]."""
+        t = self.torch
+        K = len(conds)
+        arr = (_abi.hg_trim_cond * K)()
+        for j, c in enumerate(conds):
+            config.fill_trim(arr[j], c)
+        w = None
+        if wind_ned is not None:
+            w = t.as_tensor(wind_ned, device=self.device, dtype=t.float32).contiguous()
+            if tuple(w.shape) != (K, 3):
+                raise ValueError("wind_ned must be [K, 3]")
+        out = {"state": t.empty((K, _abi.HG_N_HELI), dtype=t.float32, device=self.device),
+               "action": t.empty((K, _abi.HG_N_ACT), dtype=t.float32, device=self.device),
+               "obs": t.empty((K, _abi.HG_N_OBS), dtype=t.float32, device=self.device),
+               "status": t.full((K,), -99, dtype=t.int32, device=self.device)}
+        self._check(self.lib.hg_trim_conds_batch(self._h, arr, K, _ptr(w), _ptr(out["state"]), _ptr(out["action"]),
+                                                 _ptr(out["obs"]), _ptr(out["status"]), self._stream()))
+        return out
+
+    def set_trim_conds(self, conds):
+        """Batched set_trim_cond (helicopter.py:101-103): env i resets to the trim of conds[i] (a
+        list of N dicts).  Trims all on the device; raises if any trim fails.  `None` reverts to
+        the shared condition (set_trim_cond)."""
+        if conds is None:
+            self._check(self.lib.hg_set_reset_templates(self._h, None, self._stream()))
+            return None
+        if len(conds) != self.num_envs:
+            raise ValueError(f"need {self.num_envs} trim conditions, got {len(conds)}")
+        r = self.trim_conds(conds)
+        bad = (r["status"] != 0).nonzero().flatten()
+        if len(bad):
+            raise _abi.HeliGymError(f"trim failed for envs {bad[:10].tolist()}")
+        obs = r["obs"]
+        tmpl = self.torch.cat([r["state"], obs[:, 4:7], obs[:, 16:17], obs], dim=1).contiguous()
+        self._check(self.lib.hg_set_reset_templates(self._h, _ptr(tmpl), self._stream()))
+        return r
+
     def retrim_failures(self):
         """Auto-resets in reset_mode="retrim" whose trim did not converge (they got the template)."""
         c = ctypes.c_int64()

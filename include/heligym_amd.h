@@ -220,6 +220,20 @@ int32_t hg_rollout(hg_env* env, const float* actions_dev, int32_t nsteps, float*
 int32_t hg_trim_batch(hg_env* env, const float* wind_dev, int64_t count, float* state_dev, float* action_dev,
                       float* obs_dev, int32_t* status_dev, void* stream);
 
+/* Batched device trim for `count` trim conditions (host array `conds`, the reference's
+ * set_trim_cond dicts, helicopter.py:101-106), against `wind_dev` [count,3] fp32 or, if NULL, the
+ * mean wind: the first reset of `count` differently configured envs at once.  Outputs as
+ * hg_trim_batch.  Synchronises with `stream` before returning. */
+int32_t hg_trim_conds_batch(hg_env* env, const hg_trim_cond* conds, int64_t count, const float* wind_dev,
+                            float* state_dev, float* action_dev, float* obs_dev, int32_t* status_dev,
+                            void* stream);
+
+/* Per-env reset targets (a batched set_trim_cond): templates_dev [N,39] fp32 = trimmed heli state
+ * 18 | carry 4 (obs N/E/D velocity, ground altitude) | observation 17, one row per env, used by
+ * hg_reset and by auto-reset instead of the shared template.  NULL reverts to the shared
+ * template.  Copied; HG_RESET_TEMPLATE mode only. */
+int32_t hg_set_reset_templates(hg_env* env, const float* templates_dev, void* stream);
+
 /* Number of RETRIM-mode auto-resets so far whose trim failed (those envs got the template state).
  * Synchronises with the device. */
 int32_t hg_retrim_failures(hg_env* env, int64_t* count);
