@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--generic-kernel", action="store_true",
+                    help="step with the generic kernel instead of the default airframe's constant-specialised one")
     return ap.parse_args()
 
 
@@ -157,6 +159,8 @@ def main():
     N = args.envs
     env = HeliVecEnv(N, task=args.task, dt=args.dt, seed=1234, autoreset=True, env_offset=rank * N,
                      device=dev, reset_mode=args.reset_mode)
+    if args.generic_kernel:
+        env.set_specialized(False)
     env.reset()
 
     B = max(1, args.graph_steps)
@@ -276,6 +280,7 @@ def main():
                                f"{'hipGraph of %d steps' % B if graph is not None else 'eager'}"
                                + (", RCCL obs all-gather every step" if gathered is not None else ""),
                    "envs_per_gpu": N, "dt": args.dt, "task": args.task, "reset_mode": args.reset_mode,
+                   "kernel": "specialised (default airframe constants compiled in)" if env.specialized else "generic",
                    "parallelism": f"env-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -24,6 +24,7 @@
 #include "physics.h"
 #include "trim.h"
 #include "retrim.h"
+#include "baked.h"
 
 using hg::Params;
 using hg::Template;
@@ -106,6 +107,12 @@ using ParamArg = const Params<float>* __restrict__;
 
 #ifndef HG_MIN_WAVES
 #define HG_MIN_WAVES 1
+#endif
+#ifndef HG_MIN_WAVES_BULK   // launches with more waves than SIMDs (not NT)
+#define HG_MIN_WAVES_BULK 1
+#endif
+#ifndef HG_PREDICT_CELL
+#define HG_PREDICT_CELL 0
 #endif
 
 constexpr int kTplFloats = (int)(sizeof(Template<float>) / sizeof(float));
@@ -194,11 +201,18 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
 // their registers; MULTI: a.nsteps consecutive steps per launch (hg_rollout) with the env state
 // kept in registers between them.  All compile-time, so the hot kernel has no data-independent
 // branches to merge around.
-template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI>
-__global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
+template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
+__global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
     __shared__ float s_obs[kBlock * HG_N_OBS];
     const Params<float>& P0 = *Pa;   // model constants: scalar loads from a device copy
+    // BAKED: the default airframe's constants as instruction literals (baked.h); only the runtime
+    // fields (dt, target, limits, flags) are loaded
+    Params<float> PB;
+    if constexpr (BAKED) {
+        PB = *Pa;
+        hg::bake(PB);
+    }
     const int tid = threadIdx.x;
     const int64_t blk0 = (int64_t)blockIdx.x * kBlock;
     const int64_t i = blk0 + tid;
@@ -236,13 +250,20 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     for (int sstep = 0; sstep < nsteps; ++sstep) {
     // MULTI: the constants are re-read (scalar cache) each step rather than kept live across the
     // loop, where ~130 of them would spill out of the SGPR file
-    const Params<float>& P = MULTI ? *reload_params(Pa) : P0;
+    const Params<float>& P = BAKED ? PB : (MULTI ? *reload_params(Pa) : P0);
     const int64_t so = MULTI ? (int64_t)sstep * n : 0;   // first row of this step's inputs / outputs
     const float4 act = ld_lane(reinterpret_cast<const float4*>(a.actions) + so + blk0, lo);
     const int lane = tid & 63;
     // terrain texels under the committed position (F6): issued now, combined after the wind step
     const hg::GroundCell<float> cell_c = hg::ground_cell(P, hs[15], hs[16]);
     const hg::GroundTexels tex_c = hg::ground_fetch(a.hmap, cell_c);
+#if HG_PREDICT_CELL
+    // texels of the cell the env is predicted to end the step in (position + dt * last velocity):
+    // issued now, so the post-step ground height needs no dependent fetch unless the prediction
+    // misses (the env crosses a cell edge it was not heading for)
+    const hg::GroundCell<float> cell_p = hg::ground_cell(P, hs[15] + P.dt * carry[0], hs[16] + P.dt * carry[1]);
+    const hg::GroundTexels tex_p = hg::ground_fetch(a.hmap, cell_p);
+#endif
 
     TSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(epi), "v"(carry[3]), "v"(ws[4]));
     // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
@@ -319,7 +340,16 @@ __global__ __launch_bounds__(kBlock, HG_MIN_WAVES) void step_kernel(ParamArg Pa,
     float rew = 0.f;
     if (TASK == HG_TASK_HOVER) rew = hg::reward_hover(P, hs, k, &success_step);
     if (TASK == HG_TASK_FORWARD_FLIGHT) rew = hg::reward_forward(P, hs, k, &success_step);
+#if HG_PREDICT_CELL
+    const hg::GroundCell<float> cell_q = hg::ground_cell(P, hs[15], hs[16]);
+    hg::GroundTexels tex_q = tex_p;
+    const bool cell_miss = cell_q.mid != cell_p.mid;
+    if (hg::wave_any(cell_miss))
+        if (cell_miss) tex_q = hg::ground_fetch(a.hmap, cell_q);
+    const hg::Ground<float> h_post = hg::ground_combine<float>(tex_q, cell_q);
+#else
     const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
+#endif
     step += 1;
     const bool failed = hg::is_failed(P, hs, k, h_post);
     TSTAMP(10, "v"(rew), "v"((int)failed));
@@ -781,6 +811,8 @@ struct hg_env {
     int32_t* retrim_count = nullptr;        // [0] jobs of the current step, [1] failures so far
     float* tmpl_env = nullptr;              // per-env reset templates [N][39] (hg_set_reset_templates)
     bool env_templates = false;
+    bool baked = false;                     // step with the constant-specialised kernel (baked.h)
+    bool baked_allowed = true;              // ... unless switched off (hg_set_specialized)
     hg::TrimSetup* setup_batch = nullptr;   // hg_trim_conds_batch scratch
     int64_t setup_batch_cap = 0;
 };
@@ -790,6 +822,7 @@ static void rederive(hg_env* e) {
     e->Pd = derive<double>(e->cfg, e->rows, e->cols);
     e->Pf = derive<float>(e->cfg, e->rows, e->cols);
     e->Pf.env_templates = e->env_templates ? 1 : 0;
+    e->baked = e->baked_allowed && hg::bake_matches(e->Pf);
 }
 
 // Upload the fp32 model constants the step kernel reads (after create and every setter).
@@ -840,6 +873,28 @@ int hg_debug_timing(void* dst, int64_t bytes) {
 #endif
 
 int32_t hg_abi_version(void) { return HG_ABI_VERSION; }
+
+int32_t hg_debug_params(const hg_config* cfg, int32_t rows, int32_t cols, int32_t baked_only, void* out,
+                        int64_t bytes) {
+    if (!cfg || !out || bytes != (int64_t)sizeof(Params<float>)) return fail(HG_E_INVALID, "hg_debug_params: bad arguments");
+    const Params<float> P = derive<float>(*cfg, rows, cols);
+    if (!baked_only) {
+        memcpy(out, &P, sizeof(P));
+        return HG_OK;
+    }
+    Params<float> B;
+    memset(&B, 0, sizeof(B));
+#define HG_COPY_ONE(f) B.f = P.f;
+    HG_BAKED_FIELDS(HG_COPY_ONE)
+#undef HG_COPY_ONE
+    memcpy(out, &B, sizeof(B));
+    return HG_OK;
+}
+
+int32_t hg_config_is_baked(const hg_config* cfg, int32_t rows, int32_t cols) {
+    if (!cfg) return 0;
+    return hg::bake_matches(derive<float>(*cfg, rows, cols)) ? 1 : 0;
+}
 
 const char* hg_last_error(void) { return g_last_error.c_str(); }
 
@@ -910,8 +965,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     e->rows = rows;
     e->cols = cols;
     e->hmap_host = split_terrain(terrain_ft, rows, cols);
-    e->Pd = derive<double>(*cfg, rows, cols);
-    e->Pf = derive<float>(*cfg, rows, cols);
+    rederive(e);   // model constants, and the constant-specialised kernel when they are the baked ones
     rc = build_template(e);
     if (rc != HG_OK) { delete e; return rc; }
     auto cleanup = [&](hipError_t err, const char* what) {
@@ -986,6 +1040,13 @@ int32_t hg_set_max_time(hg_env* e, double max_time) {
     e->cfg.max_time = max_time;
     rederive(e);
     return upload_params(e);
+}
+
+int32_t hg_set_specialized(hg_env* e, int32_t enable) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    e->baked_allowed = enable != 0;
+    rederive(e);
+    return e->baked ? 1 : 0;
 }
 
 int32_t hg_set_target(hg_env* e, const hg_target* t) {
@@ -1079,11 +1140,14 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
 #define HG_LAUNCH_STEP_NT(T, NT)                                                                                 \
     do {                                                                                                         \
         if (feat) {                                                                                              \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+        } else if (NT && e->baked) {                                                                             \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, true, false, false, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, true, false, false, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
         } else {                                                                                                 \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
         }                                                                                                        \
     } while (0)
 #define HG_LAUNCH_STEP(T)                                   \
@@ -1150,11 +1214,14 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
 #define HG_LAUNCH_ROLL_NT(T, NT)                                                                                 \
     do {                                                                                                         \
         if (feat) {                                                                                              \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+        } else if (e->baked) {                                                                                   \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
         } else {                                                                                                 \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
         }                                                                                                        \
     } while (0)
 #define HG_LAUNCH_ROLL(T)                                   \

@@ -90,6 +90,7 @@ _SIGS = {
     "hg_num_envs": (ctypes.c_int64, [_P]),
     "hg_set_max_time": (ctypes.c_int32, [_P, ctypes.c_double]),
     "hg_set_target": (ctypes.c_int32, [_P, ctypes.POINTER(hg_target)]),
+    "hg_set_specialized": (ctypes.c_int32, [_P, ctypes.c_int32]),
     "hg_set_trim_cond": (ctypes.c_int32, [_P, ctypes.POINTER(hg_trim_cond)]),
     "hg_get_template": (ctypes.c_int32, [_P, ctypes.POINTER(hg_trim_result)]),
     "hg_reset": (ctypes.c_int32, [_P, _P, _P, _P]),
@@ -104,6 +105,9 @@ _SIGS = {
     "hg_trim_conds_batch": (ctypes.c_int32, [_P, ctypes.POINTER(hg_trim_cond), ctypes.c_int64, _P, _P, _P, _P,
                                              _P, _P]),
     "hg_set_reset_templates": (ctypes.c_int32, [_P, _P, _P]),
+    "hg_debug_params": (ctypes.c_int32, [ctypes.POINTER(hg_config), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                         _P, ctypes.c_int64]),
+    "hg_config_is_baked": (ctypes.c_int32, [ctypes.POINTER(hg_config), ctypes.c_int32, ctypes.c_int32]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

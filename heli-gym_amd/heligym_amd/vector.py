@@ -102,6 +102,7 @@ class HeliVecEnv:
                                           self.terrain_ft.shape[0], self.terrain_ft.shape[1],
                                           self.num_envs, ctypes.byref(h)), self.lib)
         self._h = h
+        self._specialized = bool(self.lib.hg_set_specialized(h, 1))
         N, dev = self.num_envs, self.device
         f32, u8, i32 = torch.float32, torch.uint8, torch.int32
         self.obs = torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)
@@ -207,6 +208,20 @@ class HeliVecEnv:
 
     def get_target(self):
         return dict(self._target)
+
+    def set_specialized(self, enable=True):
+        """Allow / forbid the step kernel with the default airframe's constants compiled in
+        (csrc/baked.h; bitwise-identical results).  Returns whether it is in use."""
+        rc = self.lib.hg_set_specialized(self._h, 1 if enable else 0)
+        if rc < 0:
+            self._check(rc)
+        self._specialized = bool(rc)
+        return self._specialized
+
+    @property
+    def specialized(self):
+        """True when steps run the constant-specialised kernel (the default AW109 airframe)."""
+        return self._specialized
 
     def set_trim_cond(self, trim_cond=None):
         cur = self.get_trim_cond()

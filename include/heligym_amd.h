@@ -141,6 +141,15 @@ typedef struct hg_env hg_env;
 int32_t hg_abi_version(void);
 const char* hg_last_error(void);
 
+/* Model constants of a config as the step kernel sees them (Params<float> of csrc/physics.h,
+ * `bytes` = its size), or only the fields that csrc/baked.h compiles in (`baked_only`, the rest
+ * zero).  Host only; for scripts/gen_baked_constants.py and tests. */
+int32_t hg_debug_params(const hg_config* cfg, int32_t rows, int32_t cols, int32_t baked_only, void* out,
+                        int64_t bytes);
+/* 1 when every compiled-in model constant (csrc/baked.h) equals this config's, i.e. hg_create will
+ * select the constant-specialised step kernel for it; 0 otherwise.  Host only. */
+int32_t hg_config_is_baked(const hg_config* cfg, int32_t rows, int32_t cols);
+
 /* Fill `cfg` with the AW109 / HeliHover defaults (aw109.yaml, helicopter.py:18-44,
  * helicopter_with_tasks.py:5-25).  Host only. */
 void hg_default_config(hg_config* cfg);
@@ -166,6 +175,11 @@ int64_t hg_num_envs(const hg_env* env);
  * (:101-103; re-trims the reset template).  Host only; affect subsequent device calls. */
 int32_t hg_set_max_time(hg_env* env, double max_time);
 int32_t hg_set_target(hg_env* env, const hg_target* target);
+/* Allow (1, the default) or forbid (0) the constant-specialised step kernel (csrc/baked.h), which
+ * hg_create selects when the config's model constants are the compiled-in default airframe's.
+ * Both kernels give bitwise-identical results; this switch exists for A/B timing and the tests.
+ * Returns 1 if the specialised kernel is now in use, 0 if not, or an HG_E_* code. */
+int32_t hg_set_specialized(hg_env* env, int32_t enable);
 int32_t hg_set_trim_cond(hg_env* env, const hg_trim_cond* trim);
 int32_t hg_get_template(const hg_env* env, hg_trim_result* out);
 

@@ -1,0 +1,19 @@
+# baked vs generic kernel A/B, plus GPU tests on the baked build
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_gpu.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+out=gpurun_out/exp3.jsonl; : > $out
+run() { timeout -k 10 200 python bench.py --steps 1000 --no-cpu-baseline --no-parity "$@" | python -c "import sys,json; d=json.loads(sys.stdin.read()); d['args']='${LABEL:-} $*'; print(json.dumps(d))" >> $out || { echo "bench $* failed"; exit 3; }; }
+for n in 65536 262144 1048576; do
+  run --envs $n --generic-kernel
+  run --envs $n
+  LABEL=C HELIGYM_AMD_LIB=$PWD/build/variants/C.so run --envs $n
+done
+python - <<'PY'
+import json
+for l in open("gpurun_out/exp3.jsonl"):
+    d = json.loads(l); r = d["roofline"]; ro = d.get("rollout") or {}
+    print(f'{d["args"]:40s} {d["value"]:.3e} steps/s {d["ms_per_step"]*1e3:7.2f} us/step frac {r["frac"]:.3f} kernel {d["config"]["kernel"][:11]} | rollout {ro.get("ms_per_step", 0)*1e3:6.2f} us/step')
+PY

@@ -165,3 +165,28 @@ def test_plain_c_host_runs(tmp_path):
     assert int(f["envs"]) == 4096 and int(f["resets"]) == 0
     assert abs(float(f["mean_ground_alt_ft"]) - (100 + 38.5 / 12)) < 5.0    # trimmed hover holds altitude
     assert 400 < float(f["mean_power_hp"]) < 800
+
+
+def test_baked_constants_current(lib):
+    """csrc/baked_aw109.inc (the default airframe's constants compiled into the specialised step
+    kernel) is what derive<float>() gives today: regenerate with scripts/gen_baked_constants.py."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_baked", os.path.join(ROOT, "scripts", "gen_baked_constants.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    assert open(gen.OUT).read() == gen.current_text()
+
+
+@pytest.mark.parametrize("kw,baked", [(dict(), True), (dict(dt=0.02), True), (dict(task="forward_flight"), True),
+                                      (dict(max_time=20.0, target={"sea_alt": 3000.0}), True),
+                                      (dict(turbulence_level=5), False), (dict(variant="heavy"), False),
+                                      (dict(variant="turb7_wind"), False)])
+def test_specialised_kernel_selection(lib, kw, baked):
+    """The specialised kernel is selected for the default airframe whatever the dt, task, target or
+    time limit (those stay runtime values), and for nothing else."""
+    if "variant" in kw:
+        cfg, _ = config.make_config(heli_name=golden_cases.load_variant(kw["variant"])[1])
+    else:
+        cfg, _ = config.make_config(**kw)
+    assert lib.hg_config_is_baked(ctypes.byref(cfg), 1024, 1024) == (1 if baked else 0)
+    assert lib.hg_config_is_baked(ctypes.byref(cfg), 512, 512) == 0   # other terrain size

@@ -713,3 +713,37 @@ def test_per_env_trim_conditions(torch):
     obs, _ = env.reset()
     np.testing.assert_allclose(obs.cpu().numpy(), np.tile(env.template()["obs"].astype(np.float32), (N, 1)))
     env.close()
+
+
+@pytest.mark.parametrize("task", ["hover", "forward_flight"])
+def test_specialised_kernel_bitwise_equals_generic(torch, task):
+    """The default airframe's constant-specialised kernel (csrc/baked.h: the model constants as
+    instruction literals) and the generic kernel (constants loaded from the device copy) give
+    bitwise-identical steps and rollouts: random actions, in-kernel turbulence, auto-resets."""
+    N, K, R = 4096, 300, 50
+
+    def run(spec):
+        env = make_env(torch, N, task, 0.01, autoreset=True, seed=3)
+        assert env.set_specialized(spec) == spec
+        env.reset()
+        act = torch.empty((N, 4), dtype=torch.float32, device=env.device)
+        rew_sum = torch.zeros((N,), dtype=torch.float32, device=env.device)
+        flags = torch.zeros((N,), dtype=torch.int32, device=env.device)
+        for k in range(K):
+            env.random_actions(act, seed=9, step=k)
+            env.step_async(act, with_reset_info=False)
+            rew_sum += torch.nan_to_num(env.reward, nan=0.0)
+            flags += env.terminated_u8.int() + 2 * env.truncated_u8.int()
+        bank = torch.empty((R, N, 4), dtype=torch.float32, device=env.device)
+        for k in range(R):
+            env.random_actions(bank[k], seed=10, step=k)
+        ro = env.rollout(bank)
+        s, c = env.get_state()
+        res = [x.cpu().numpy().copy() for x in (env.obs, rew_sum, flags, s, c, *ro)]
+        env.close()
+        return res
+
+    a, b = run(True), run(False)
+    assert int(a[2].sum()) > 0   # some episodes ended (auto-reset exercised)
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
