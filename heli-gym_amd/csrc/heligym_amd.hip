@@ -158,21 +158,48 @@ __device__ __forceinline__ void st_lane(T* base, uint32_t idx, T v) {
 // Observations of a step: each wave stages its 64 rows in its own LDS slice (stride 17 is
 // bank-conflict free) and writes them back as contiguous float4, with no block-wide barrier.
 template <bool NT>
-__device__ __forceinline__ void store_obs(float* s_obs, const float obs[17], float* dst, int64_t so, int64_t blk0,
-                                          int64_t n, int tid) {
-    const int lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
-    float* w_obs = s_obs + wv * 64 * HG_N_OBS;
+__device__ __forceinline__ void store_obs_wave(float* w_obs, const float obs[17], float* dst, int64_t so, int64_t w0,
+                                               int64_t n, int lane) {
 #pragma unroll
     for (int c = 0; c < 17; ++c) w_obs[lane * 17 + c] = obs[c];
     __builtin_amdgcn_wave_barrier();
-    const int64_t w0 = blk0 + wv * 64;
     const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
     const int cnt = nw > 0 ? nw * 17 : 0;
     float* out = dst + (so + w0) * 17;
     const int n4 = cnt >> 2;
     for (int j = lane; j < n4; j += 64) st_out4<NT>(out + 4 * j, w_obs + 4 * j);
     for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
+}
+
+template <bool NT>
+__device__ __forceinline__ void store_obs(float* s_obs, const float obs[17], float* dst, int64_t so, int64_t blk0,
+                                          int64_t n, int tid) {
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
+    store_obs_wave<NT>(s_obs + wv * 64 * HG_N_OBS, obs, dst, so, blk0 + wv * 64, n, tid & 63);
+}
+
+// Turbulence noise of a step (wind_dynamics.py:49-52: eta = randn(3) / sqrt(dt)): injected by the
+// caller (ETA), or Box-Muller normals from Philox4x32-10 keyed by (global env id, step, episode).
+template <bool ETA>
+__device__ __forceinline__ void draw_eta(const StepArgs& a, const Params<float>& P, int64_t so, int64_t blk0,
+                                         uint32_t lo, int32_t step, int32_t epi, float eta[3]) {
+    if (ETA) {
+        const float* eb = a.eta + 3 * (so + blk0);
+        eta[0] = ld_lane(eb + 0, 3 * lo);
+        eta[1] = ld_lane(eb + 1, 3 * lo);
+        eta[2] = ld_lane(eb + 2, 3 * lo);
+    } else {
+        const uint64_t gid = (uint64_t)(a.env_offset + blk0 + lo);
+        const U4 r = philox(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)epi},
+                            (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+        float sn, cs;
+        const float r0 = sqrtf(-2.f * __logf(u01(r.x)));
+        __sincosf(6.28318530717958648f * u01(r.y), &sn, &cs);
+        const float r1 = sqrtf(-2.f * __logf(u01(r.z)));
+        eta[0] = r0 * cs * P.eta_norm;
+        eta[1] = r0 * sn * P.eta_norm;
+        eta[2] = r1 * __cosf(6.28318530717958648f * u01(r.w)) * P.eta_norm;
+    }
 }
 
 // Diagnostic build only: per-wave phase timestamps (s_memtime) of one launch, for latency
@@ -191,8 +218,17 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
         const int w_ = (int)(i >> 6);                                                           \
         if ((tid & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;                      \
     } while (0)
+// two-wave kernel: slot row per wave (block * 2 + role)
+#define PSTAMP(j, ...)                                                                          \
+    do {                                                                                        \
+        asm volatile("" ::__VA_ARGS__);                                                         \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+        const int w_ = (int)(blockIdx.x * 2 + (tid >> 6));                                      \
+        if (lane == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;                            \
+    } while (0)
 #else
 #define TSTAMP(j, ...) do { } while (0)
+#define PSTAMP(j, ...) do { } while (0)
 #endif
 
 // TASK: reward / success of the task; ETA: noise injected by the caller (else in-kernel Philox);
@@ -268,23 +304,7 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     TSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(epi), "v"(carry[3]), "v"(ws[4]));
     // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
     float eta[3];
-    if (ETA) {
-        const float* eb = a.eta + 3 * (so + blk0);
-        eta[0] = ld_lane(eb + 0, 3 * lo);
-        eta[1] = ld_lane(eb + 1, 3 * lo);
-        eta[2] = ld_lane(eb + 2, 3 * lo);
-    } else {
-        const uint64_t gid = (uint64_t)(a.env_offset + blk0 + lo);
-        const U4 r = philox(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)epi},
-                            (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
-        float sn, cs;
-        const float r0 = sqrtf(-2.f * __logf(u01(r.x)));
-        __sincosf(6.28318530717958648f * u01(r.y), &sn, &cs);
-        const float r1 = sqrtf(-2.f * __logf(u01(r.z)));
-        eta[0] = r0 * cs * P.eta_norm;
-        eta[1] = r0 * sn * P.eta_norm;
-        eta[2] = r1 * __cosf(6.28318530717958648f * u01(r.w)) * P.eta_norm;
-    }
+    draw_eta<ETA>(a, P, so, blk0, lo, step, epi, eta);
 
     // ground height under the committed position (F6), wind step (Heli.step :195-199)
     TSTAMP(2, "v"(eta[2]), "v"(eta[0]));
@@ -455,6 +475,255 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     __builtin_amdgcn_s_waitcnt(0);
     TSTAMP(12, "v"(tid));
     if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][14] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
+// ------------------------------------------------------------------------------ two-wave step
+// step_kernel's step for launches of at most one wave per SIMD (N <= 64 x 4 x CUs; 65 536 envs on
+// MI355X) with the default airframe's constants compiled in.  At one wave per SIMD the step is
+// bound by that wave's single instruction stream: one wave issues a VALU every ~4-5 cycles while
+// its SIMD can take one every ~2.5 from two waves (MI355X_MICROARCH.md, 'vector-instruction ISSUE
+// cost'; scripts/ubench/issue.hip).  Here every 64 envs get two waves (a 128-thread block), one
+// env per lane in each, and the work of the step is split between them:
+//   * the rotor wave (0) draws the noise and steps the wind; the airframe wave (1) takes the
+//     sines and cosines of the committed attitude;
+//   * every RK stage, both evaluate the kinematics (hg::frame) and the equations of motion
+//     (hg::eom), so both hold the full state, while the rotor wave evaluates the main rotor and
+//     fuselage (hg::main_loads) and the airframe wave the tail rotor, tails, wing and gear
+//     (hg::tail_loads); the two trade their 10 + 10 terms through LDS around one block barrier;
+//   * after the step the rotor wave computes the reward and the airframe wave the post-step ground
+//     height and failure test; the stores are split by column.
+// Same physics.h parts in the same order as step_kernel: the results are bitwise identical
+// (tests/test_gpu_parity.py::test_specialised_kernel_bitwise_equals_generic).
+constexpr int kPairBlock = 128;
+constexpr int kLoadTerms = 10;   // hg::Loads<float>: d[3], F[3], M[3], power
+
+__device__ __forceinline__ void put_loads(float (*x)[64], int l, const hg::Loads<float>& o) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        x[j][l] = o.d[j];
+        x[3 + j][l] = o.F[j];
+        x[6 + j][l] = o.M[j];
+    }
+    x[9][l] = o.power;
+}
+
+__device__ __forceinline__ hg::Loads<float> get_loads(const float (*x)[64], int l) {
+    hg::Loads<float> o;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        o.d[j] = x[j][l];
+        o.F[j] = x[3 + j][l];
+        o.M[j] = x[6 + j][l];
+    }
+    o.power = x[9][l];
+    return o;
+}
+
+template <int TASK, bool ETA, bool MULTI>
+__global__ __launch_bounds__(kPairBlock, 2) void pair_step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
+                                                                const StepArgs a) {
+    __shared__ float x_main[2][kLoadTerms][64];   // rotor wave -> airframe wave, by RK-stage parity
+    __shared__ float x_tail[2][kLoadTerms][64];   // airframe wave -> rotor wave
+    __shared__ float x_wind[3][64];               // wind of the step (rotor -> airframe)
+    __shared__ float x_att[6][64];                // sin / cos of the committed attitude (airframe -> rotor)
+    __shared__ int32_t x_flag[2][64];             // success_step (rotor), failed (airframe)
+    __shared__ float s_obs[64 * HG_N_OBS];        // airframe wave's observation staging
+    Params<float> P = *Pa;
+    hg::bake(P);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const bool rotor = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;   // wave-uniform role
+    const int64_t blk0 = (int64_t)blockIdx.x * 64;
+    const int64_t i = blk0 + lane;
+    const int64_t n = a.n;
+    const bool active = i < n;
+    const uint32_t lo = (uint32_t)(active ? lane : 0);
+    float* st_b = a.state + blk0;
+    int32_t* ct_b = a.counters + blk0;
+#if HG_TIMING
+    if (lane == 0 && blockIdx.x * 2 + (tid >> 6) < HG_TIMING_WAVES)
+        g_timing[blockIdx.x * 2 + (tid >> 6)][15] = __builtin_amdgcn_s_memrealtime();
+#endif
+    PSTAMP(0, "v"(tid));
+
+    float hs[18], ws[5], carry[4];
+    hs[15] = ld_lane(COL(st_b, 15), lo);
+    hs[16] = ld_lane(COL(st_b, 16), lo);
+    int32_t step = ld_lane(COL(ct_b, 0), lo), succ = ld_lane(COL(ct_b, 1), lo), epi = ld_lane(COL(ct_b, 2), lo);
+    if (rotor) {
+#pragma unroll
+        for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lo);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lo);
+#pragma unroll
+    for (int c = 0; c < 18; ++c)
+        if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lo);
+    const int nsteps = MULTI ? a.nsteps : 1;
+    for (int sstep = 0; sstep < nsteps; ++sstep) {
+        const int64_t so = MULTI ? (int64_t)sstep * n : 0;
+        const float4 act = ld_lane(reinterpret_cast<const float4*>(a.actions) + so + blk0, lo);
+        const hg::GroundCell<float> cell_c = hg::ground_cell(P, hs[15], hs[16]);
+        const hg::GroundTexels tex_c = hg::ground_fetch(a.hmap, cell_c);
+        PSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(carry[3]));
+        float W[3];
+        hg::Attitude<float> att0;
+        if (rotor) {   // noise and wind step (Heli.step :195-199)
+            float eta[3];
+            draw_eta<ETA>(a, P, so, blk0, lo, step, epi, eta);
+            hg::wind_step(P, ws, carry, eta, W);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) x_wind[j][lane] = W[j];
+        } else {
+            att0 = hg::attitude(hs + 12);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                x_att[j][lane] = att0.s[j];
+                x_att[3 + j][lane] = att0.c[j];
+            }
+        }
+        PSTAMP(2, "v"(tid));
+        __syncthreads();
+        PSTAMP(3, "v"(tid));
+        if (rotor) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                att0.s[j] = x_att[j][lane];
+                att0.c[j] = x_att[3 + j][lane];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) W[j] = x_wind[j][lane];
+        }
+        const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
+
+        // RK4 (dynamics.py:158-171) with the loads of each stage split over the two waves
+        const hg::Controls<float> u = hg::controls(P, act.x, act.y, act.z, act.w);
+        float k[18], acc[18], st[18], obs[17];
+        const float e0[3] = {hs[12], hs[13], hs[14]};
+#pragma unroll
+        for (int stg = 0; stg < 4; ++stg) {
+            const float* si = stg == 0 ? hs : st;
+            const hg::Attitude<float> att = stg == 0 ? att0 : hg::attitude_step(att0, e0, st + 12);
+            const hg::Frame<float> f = hg::frame(P, si, W, h_c, att);
+            hg::Loads<float> A, B;
+            if (rotor) {
+                A = hg::main_loads(P, si, u, f);
+                put_loads(x_main[stg & 1], lane, A);
+            } else {
+                B = hg::tail_loads(P, si, u, f);
+                put_loads(x_tail[stg & 1], lane, B);
+            }
+            PSTAMP(4 + 2 * stg, "v"(tid));
+            __syncthreads();
+            PSTAMP(5 + 2 * stg, "v"(tid));
+            if (rotor) B = get_loads(x_tail[stg & 1], lane);
+            else A = get_loads(x_main[stg & 1], lane);
+            hg::eom(P, si, f, A, B, k);
+            if (stg == 3) hg::observe(P, si, f, A, B, obs);
+            if (stg == 0) {
+#pragma unroll
+                for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
+            } else if (stg == 1) {
+#pragma unroll
+                for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
+            } else if (stg == 2) {
+#pragma unroll
+                for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.dt; }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
+            }
+        }
+        const float tpl = lane < kTplFloats ? reinterpret_cast<const float*>(Tp)[lane] : 0.f;
+        // step_after (helicopter_dynamics.py:73-77)
+        hs[2] = hg::pi_bound(hs[2]);
+        hs[3] = hg::pi_bound(hs[3]);
+        hs[4] = hg::pi_bound(hs[4]);
+        hs[5] = hg::pi_bound(hs[5]);
+        hs[12] = hg::pi_bound(hs[12]);
+        hs[13] = hg::pi_bound(hs[13]);
+        hs[14] = hg::pi_bound(hs[14]);
+
+        // reward (rotor wave) and failure test (airframe wave), exchanged
+        bool success_step = false, failed = false;
+        float rew = 0.f;
+        if (rotor) {
+            if (TASK == HG_TASK_HOVER) rew = hg::reward_hover(P, hs, k, &success_step);
+            if (TASK == HG_TASK_FORWARD_FLIGHT) rew = hg::reward_forward(P, hs, k, &success_step);
+            x_flag[0][lane] = success_step ? 1 : 0;
+        } else {
+            const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
+            failed = hg::is_failed(P, hs, k, h_post);
+            x_flag[1][lane] = failed ? 1 : 0;
+        }
+        PSTAMP(12, "v"(hs[0]), "v"(rew));
+        __syncthreads();
+        if (rotor) failed = x_flag[1][lane] != 0;
+        else success_step = x_flag[0][lane] != 0;
+        step += 1;
+        const bool successed = succ >= P.success_steps;   // successed_time before this step's add
+        const bool time_up = step >= P.time_up_steps;
+        const bool term = failed || successed;
+        const bool trunc = time_up;
+        const bool done = term || trunc;
+        succ += success_step ? 1 : 0;
+        const bool do_reset = P.autoreset && active && done;
+        if (rotor) {
+            if (active) st_lane<true>(a.reward + so + blk0, (uint32_t)lane, rew);
+        } else if (active) {
+            st_lane<true>(a.terminated + so + blk0, (uint32_t)lane, (uint8_t)term);
+            st_lane<true>(a.truncated + so + blk0, (uint32_t)lane, (uint8_t)trunc);
+            if (a.info)
+                st_lane<true>(a.info + so + blk0, (uint32_t)lane,
+                              (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
+                                        (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0)));
+        }
+        // same-step auto-reset from the template, float c held by lane c (heli 18 | carry 4 | obs 17)
+        if (do_reset) {
+#pragma unroll
+            for (int c = 0; c < 18; ++c) hs[c] = lane_value(tpl, c);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) carry[c] = lane_value(tpl, 18 + c);
+#pragma unroll
+            for (int c = 0; c < 17; ++c) obs[c] = lane_value(tpl, 22 + c);
+#pragma unroll
+            for (int c = 0; c < 5; ++c) ws[c] = 0.f;
+            step = 0;
+            succ = 0;
+            epi += 1;
+        } else {
+            carry[0] = obs[4];
+            carry[1] = obs[5];
+            carry[2] = obs[6];
+            carry[3] = obs[16];
+        }
+        if (!rotor) store_obs_wave<true>(s_obs, obs, a.obs, so, blk0, n, lane);
+    }   // steps
+    // state: heli + wind by the rotor wave, carry + counters by the airframe wave
+    st_b = a.state + blk0;
+    ct_b = a.counters + blk0;
+    asm volatile("" : "+s"(st_b), "+s"(ct_b));
+    if (active) {
+        if (rotor) {
+#pragma unroll
+            for (int c = 0; c < 18; ++c) st_lane<true>(COL(st_b, c), (uint32_t)lane, hs[c]);
+#pragma unroll
+            for (int c = 0; c < 5; ++c) st_lane<true>(COL(st_b, 18 + c), (uint32_t)lane, ws[c]);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) st_lane<true>(COL(st_b, 23 + c), (uint32_t)lane, carry[c]);
+            st_lane<true>(COL(ct_b, 0), (uint32_t)lane, step);
+            st_lane<true>(COL(ct_b, 1), (uint32_t)lane, succ);
+            st_lane<true>(COL(ct_b, 2), (uint32_t)lane, epi);
+        }
+    }
+#if HG_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    PSTAMP(13, "v"(tid));
+    if (lane == 0 && blockIdx.x * 2 + (tid >> 6) < HG_TIMING_WAVES)
+        g_timing[blockIdx.x * 2 + (tid >> 6)][14] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
@@ -865,6 +1134,22 @@ static inline unsigned retrim_grid(int64_t jobs) {
 
 #define PARAM_ARG(e) ((const Params<float>*)(e)->params_dev)
 
+// The default airframe's constant-specialised step for launches of at most one wave per SIMD:
+// the two-wave kernel (HG_PAIR, default), or step_kernel<..., BAKED> (diagnostic builds, A/B).
+#ifndef HG_PAIR
+#define HG_PAIR 1
+#endif
+static inline unsigned pair_grid(int64_t n) { return (unsigned)((n + 63) / 64); }
+#if HG_PAIR
+#define HG_LAUNCH_SPECIALISED(T, ETA_, MULTI_)                                                             \
+    hipLaunchKernelGGL((pair_step_kernel<T, ETA_, MULTI_>), dim3(pair_grid(e->n)), dim3(kPairBlock), 0, s, \
+                       PARAM_ARG(e), e->tmpl_dev, a)
+#else
+#define HG_LAUNCH_SPECIALISED(T, ETA_, MULTI_)                                                             \
+    hipLaunchKernelGGL((step_kernel<T, ETA_, true, false, MULTI_, true>), grid, block, 0, s, PARAM_ARG(e), \
+                       e->tmpl_dev, a)
+#endif
+
 extern "C" {
 #if HG_TIMING
 int hg_debug_timing(void* dst, int64_t bytes) {
@@ -1143,8 +1428,8 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
         } else if (NT && e->baked) {                                                                             \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, true, false, false, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, true, false, false, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) HG_LAUNCH_SPECIALISED(T, true, false);                                                      \
+            else HG_LAUNCH_SPECIALISED(T, false, false);                                                         \
         } else {                                                                                                 \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
@@ -1216,9 +1501,9 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
         if (feat) {                                                                                              \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
-        } else if (e->baked) {                                                                                   \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, true>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+        } else if (NT && e->baked) {                                                                             \
+            if (eta) HG_LAUNCH_SPECIALISED(T, true, true);                                                       \
+            else HG_LAUNCH_SPECIALISED(T, false, true);                                                          \
         } else {                                                                                                 \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \

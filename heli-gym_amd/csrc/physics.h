@@ -66,8 +66,10 @@ HD Attitude<R> attitude(const R* eul) {
 }
 
 // Attitude of a RK stage from the committed attitude: sin/cos(e + d) by the angle-addition
-// formulas with short Taylor series for the stage increment d (|d| <= 0.25 rad: truncation
-// < 2e-8); a lane with a larger increment (a tumbling, diverging env) takes the full sincos.
+// formulas with short Taylor series for the stage increment d.  For |d| <= 0.05 rad (attitude
+// rates below 5 rad/s at dt 0.01, 2.5 rad/s at dt 0.02) sin d = d - d^3/6 and
+// cos d = 1 - d^2/2 + d^4/24 are within 2.7e-9 and 2.2e-11; a lane with a larger increment (a
+// tumbling, diverging env) takes the full sincos.
 template <typename R>
 HD Attitude<R> attitude_step(const Attitude<R>& a0, const R* eul0, const R* eul) {
     Attitude<R> a;
@@ -77,9 +79,9 @@ HD Attitude<R> attitude_step(const Attitude<R>& a0, const R* eul0, const R* eul)
     for (int j = 0; j < 3; ++j) {
         const R d = eul[j] - eul0[j];
         const R d2 = d * d;
-        big = big || !(m_fabs(d) <= (R)0.25);
-        sd[j] = d * ((R)1 - d2 * (R)(1.0 / 6.0) * ((R)1 - d2 * (R)(1.0 / 20.0)));
-        cd[j] = (R)1 - d2 * (R)0.5 * ((R)1 - d2 * (R)(1.0 / 12.0) * ((R)1 - d2 * (R)(1.0 / 30.0)));
+        big = big || !(m_fabs(d) <= (R)0.05);
+        sd[j] = d + (d * d2) * (R)(-1.0 / 6.0);
+        cd[j] = (R)1 + d2 * ((R)-0.5 + d2 * (R)(1.0 / 24.0));
     }
     if (big) return attitude(eul);
 #pragma unroll
@@ -177,6 +179,8 @@ struct Template {
 template <typename R>
 struct Controls {
     R coll, lon, lat, ped;
+    // the control-only parts of the rotors' blade-relative inflow (:226, :281), fixed over a step
+    R mr_wb0, mr_wb1, tr_vb0, tr_vb1;
 };
 
 // helicopter_dynamics.py:414-422 (no clipping of the action, like the reference).
@@ -187,6 +191,10 @@ HD Controls<R> controls(const Params<R>& P, R a0, R a1, R a2, R a3) {
     u.lon = P.lon0 + P.lon1 * a1;
     u.lat = P.lat0 + P.lat1 * a2;
     u.ped = P.ped0 + P.ped1 * a3;
+    u.mr_wb0 = P.mr_two3_vtip * (u.coll + P.mr_tw75);
+    u.mr_wb1 = P.mr_inv_VTIP * (u.coll + P.mr_tw50);
+    u.tr_vb0 = P.tr_two3_vtip * (u.ped + P.tr_tw75);
+    u.tr_vb1 = P.tr_inv_VTIP * (u.ped + P.tr_tw50);
     return u;
 }
 
@@ -444,17 +452,29 @@ HD void wind_step(const Params<R>& P, R s[5], const R carry[4], const R eta[3],
 }
 
 // ------------------------------------------------------------------------------------------
-// HelicopterDynamics.dynamics (helicopter_dynamics.py:400-489).
-// s: [vi_mr vi_tr psi_mr psi_tr b0 b1 u v w p q r phi theta psi x y z]; W: wind NED; h_c: ground
-// height under the COMMITTED position (F6).  Writes d[18]; with OBS also the 17 observations.
-template <bool OBS, typename R>
-HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>& u, const R W[3],
-                 const Ground<R>& gc, const Attitude<R>& att, R* __restrict__ d, R* __restrict__ obs) {
-    const R vi_mr = s[0], vi_tr = s[1], b0 = s[4], b1 = s[5];
-    const R uu = s[6], vv = s[7], ww = s[8], p = s[9], q = s[10], r = s[11];
-    const R phi = s[12], th = s[13], psi = s[14];
-    const R z = s[17];
+// HelicopterDynamics.dynamics (helicopter_dynamics.py:400-489), in parts: the kinematics every
+// force model uses (frame), two groups of component models (main_loads: main rotor + fuselage;
+// tail_loads: tail rotor, tails, wing, landing gear), and the equations of motion (eom) that add
+// the two groups.  dynamics() chains them for one lane; the two-wave step kernel evaluates the two
+// groups on different waves.  Same arithmetic either way, so the results are bitwise identical.
+// s: [vi_mr vi_tr psi_mr psi_tr b0 b1 u v w p q r phi theta psi x y z]; W: wind NED; gc: ground
+// height under the COMMITTED position (F6).
 
+// Stage-input kinematics (:423-445, kinematic.py:3-29, ISA density :160-165).
+template <typename R>
+struct Frame {
+    R B02, B12, B22;     // third column of the earth->body DCM (gravity, landing gear)
+    R phid, thd, psid;   // euler rates
+    R n0, n1, n2;        // NED velocity B^T uvw
+    R ua, va, wa;        // air-relative body velocity uvw - B W
+    R rho, irho;         // density at -z and its reciprocal
+    R zh;                // z + h under the committed position
+};
+
+template <typename R>
+HD Frame<R> frame(const Params<R>& P, const R* __restrict__ s, const R W[3], const Ground<R>& gc,
+                  const Attitude<R>& att) {
+    const R uu = s[6], vv = s[7], ww = s[8], p = s[9], q = s[10], r = s[11];
     // kinematic.py:3-29: B = earth->body DCM, T = pqr->euler rate
     const R s0 = att.s[0], c0 = att.c[0], s1 = att.s[1], c1 = att.c[1], s2 = att.s[2], c2 = att.c[2];
     const R B00 = c1 * c2, B01 = c1 * s2, B02 = -s1;
@@ -463,23 +483,44 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
     const R B20 = c0s1 * c2 + s0 * s2, B21 = c0s1 * s2 - s0 * c2, B22 = c0 * c1;
     const R ic1 = m_rcp(c1);
     const R t1 = s1 * ic1;
-    const R phid = p + (s0 * t1) * q + (c0 * t1) * r;
-    const R thd = c0 * q - s0 * r;
-    const R psid = (s0 * ic1) * q + (c0 * ic1) * r;
+    Frame<R> f;
+    f.B02 = B02;
+    f.B12 = B12;
+    f.B22 = B22;
+    f.phid = p + (s0 * t1) * q + (c0 * t1) * r;
+    f.thd = c0 * q - s0 * r;
+    f.psid = (s0 * ic1) * q + (c0 * ic1) * r;
     // ned = B^T uvw, uvw_air = uvw - B W (:428-431)
-    const R n0 = B00 * uu + B10 * vv + B20 * ww;
-    const R n1 = B01 * uu + B11 * vv + B21 * ww;
-    const R n2 = B02 * uu + B12 * vv + B22 * ww;
-    const R ua = uu - (B00 * W[0] + B01 * W[1] + B02 * W[2]);
-    const R va = vv - (B10 * W[0] + B11 * W[1] + B12 * W[2]);
-    const R wa = ww - (B20 * W[0] + B21 * W[1] + B22 * W[2]);
-    const R power_climb = P.wt * (-n2);
-    // ISA density at altitude -z (:160-165)
-    const R rho = P.ro_sea * m_pow((R)1 + P.lapse_t0 * z, P.rho_exp);
+    f.n0 = B00 * uu + B10 * vv + B20 * ww;
+    f.n1 = B01 * uu + B11 * vv + B21 * ww;
+    f.n2 = B02 * uu + B12 * vv + B22 * ww;
+    f.ua = uu - (B00 * W[0] + B01 * W[1] + B02 * W[2]);
+    f.va = vv - (B10 * W[0] + B11 * W[1] + B12 * W[2]);
+    f.wa = ww - (B20 * W[0] + B21 * W[1] + B22 * W[2]);
+    f.rho = P.ro_sea * m_pow((R)1 + P.lapse_t0 * s[17], P.rho_exp);
+    f.irho = m_rcp(f.rho);
+    // z + h with the large cancellation first (Ground::zh): the stiff gear spring K * (pos_z + h)
+    // keeps its precision near the ground
+    f.zh = gc.zh(s[17]);
+    return f;
+}
 
-    // ---- main rotor (:203-270)
-    const R gam = rho * P.mr_gam_dro;
-    const R irho = m_rcp(rho);
+// Forces, moments and power of a group of components, and the derivatives of the states the group
+// owns (main: vi_mr, b0, b1; tail: vi_tr).
+template <typename R>
+struct Loads {
+    R d[3];
+    R F[3], M[3];
+    R power;
+};
+
+// Main rotor (:203-270) and fuselage (:302-320).
+template <typename R>
+HD Loads<R> main_loads(const Params<R>& P, const R* __restrict__ s, const Controls<R>& u, const Frame<R>& f) {
+    const R vi_mr = s[0], b0 = s[4], b1 = s[5], p = s[9], q = s[10];
+    const R ua = f.ua, va = f.va, wa = f.wa, rho = f.rho, irho = f.irho;
+    Loads<R> o;
+    // ---- main rotor
     const R igam = irho * P.mr_inv_gam_dro;
     const R KC = P.mr_kc_num * igam + P.mr_K1;
     const R og = P.mr_OMEGA * igam;
@@ -488,10 +529,10 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
     const R DL_DA1 = rho * P.mr_DL_DA1_dro;
     const R vadv2 = ua * ua + va * va;
     const R wr = wa + (b0 - P.mr_IS) * ua - b1 * va;
-    const R wb = wr + P.mr_two3_vtip * (u.coll + P.mr_tw75) + vadv2 * P.mr_inv_VTIP * (u.coll + P.mr_tw50);
+    const R wb = wr + u.mr_wb0 + vadv2 * u.mr_wb1;
     const R thr = (wb - vi_mr) * rho * P.mr_coef;
     const R dw = wr - vi_mr;
-    d[0] = P.mr_inflow * (thr * irho * P.mr_inv_thr_den - vi_mr * m_sqrt(vadv2 + dw * dw));
+    o.d[0] = P.mr_inflow * (thr * irho * P.mr_inv_thr_den - vi_mr * m_sqrt(vadv2 + dw * dw));
     const R power_mr = thr * (vi_mr - wr) + rho * P.mr_prof * (P.mr_vtip2 + (R)3 * vadv2);
     R CT = thr * irho * P.mr_inv_ct_den;
     CT = CT > (R)0 ? CT : (R)0;
@@ -499,25 +540,12 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
     const R wake = m_fabs(ua) > P.vtrans ? (R)1 : (R)0;
     const R a_sum = b1 - u.lat + KC * b0 + DB1DV * va * ((R)1 + wake);
     const R b_sum = b0 + u.lon - KC * b1 - DB1DV * ua * ((R)1 + (R)2 * wake);
-    d[4] = -ITB * b_sum - ITB2_OM * a_sum - q;
-    d[5] = -ITB * a_sum + ITB2_OM * b_sum - p;
-    d[2] = P.mr_OMEGA;
+    o.d[1] = -ITB * b_sum - ITB2_OM * a_sum - q;
+    o.d[2] = -ITB * a_sum + ITB2_OM * b_sum - p;
     const R X_MR = -thr * (b0 - P.mr_IS), Y_MR = thr * b1, Z_MR = -thr;
     const R L_MR = Y_MR * P.mr_H + P.mr_DL_DB1 * b1 + DL_DA1 * (b0 + u.lon - P.mr_K1 * b1);
     const R M_MR = Z_MR * P.mr_D - X_MR * P.mr_H + P.mr_DL_DB1 * b0 + DL_DA1 * (-b1 + u.lat - P.mr_K1 * b0);
-
-    // ---- tail rotor (:272-300)
-    const R wq = wa + q * P.tr_D;
-    const R vadv2t = wq * wq + ua * ua;
-    const R vr = -(va - r * P.tr_D + p * P.tr_H);
-    const R vb = vr + P.tr_two3_vtip * (u.ped + P.tr_tw75) + vadv2t * P.tr_inv_VTIP * (u.ped + P.tr_tw50);
-    const R thr_t = (vb - vi_tr) * rho * P.tr_coef;
-    const R dwt = vr - vi_tr;
-    d[1] = P.tr_inflow * (thr_t * irho * P.tr_inv_thr_den - vi_tr * m_sqrt(vadv2t + dwt * dwt));
-    d[3] = P.tr_OMEGA;
-    const R power_tr = thr_t * (vi_tr - vr);
-
-    // ---- fuselage (:302-320)
+    // ---- fuselage
     R wa_f = wa - vi_mr;
     wa_f = wa_f > (R)0 ? wa_f + (R)kEps : wa_f;
     const R d_fw = ((ua * m_rcp(-wa_f)) * P.fus_dfw_k - P.fus_dfw_c) * P.fus_COR;
@@ -526,8 +554,39 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
     const R Y_F = rh * P.fus_YVV * m_fabs(va) * va;
     const R Z_F = rh * P.fus_ZWW * m_fabs(wa_f) * wa_f;
     const R power_fus = -X_F * ua - Y_F * va - Z_F * wa_f;
+    // climb and fuselage power load the main rotor's torque (:446-447)
+    const R power_climb = P.wt * (-f.n2);
+    const R p_extra = power_climb + power_fus;
+    o.F[0] = X_MR + X_F;
+    o.F[1] = Y_MR + Y_F;
+    o.F[2] = Z_MR + Z_F;
+    o.M[0] = L_MR + Y_F * P.fus_H;
+    o.M[1] = M_MR + (Z_F * d_fw - X_F * P.fus_H);
+    o.M[2] = power_mr * P.mr_inv_OMEGA + p_extra * P.mr_inv_OMEGA;
+    o.power = power_mr + p_extra;
+    return o;
+}
 
-    // ---- horizontal tail (:322-345)
+// Tail rotor (:272-300), horizontal tail (:322-345), vertical tail (:347-361), wing (:363-383),
+// landing gear (:385-398).
+template <typename R>
+HD Loads<R> tail_loads(const Params<R>& P, const R* __restrict__ s, const Controls<R>& u, const Frame<R>& f) {
+    const R vi_mr = s[0], vi_tr = s[1], p = s[9], q = s[10], r = s[11];
+    const R ua = f.ua, va = f.va, wa = f.wa, rho = f.rho, irho = f.irho;
+    Loads<R> o;
+    // ---- tail rotor
+    const R wq = wa + q * P.tr_D;
+    const R vadv2t = wq * wq + ua * ua;
+    const R vr = -(va - r * P.tr_D + p * P.tr_H);
+    const R vb = vr + u.tr_vb0 + vadv2t * u.tr_vb1;
+    const R thr_t = (vb - vi_tr) * rho * P.tr_coef;
+    const R dwt = vr - vi_tr;
+    o.d[0] = P.tr_inflow * (thr_t * irho * P.tr_inv_thr_den - vi_tr * m_sqrt(vadv2t + dwt * dwt));
+    o.d[1] = (R)0;
+    o.d[2] = (R)0;
+    const R power_tr = thr_t * (vi_tr - vr);
+    const R rh = (R)0.5 * rho;
+    // ---- horizontal tail
     const R v_dw = m_max(vi_mr - wa, (R)kEps);
     const R d_dw = ua * m_rcp(v_dw) * P.ht_dw_k - P.ht_dw_c;
     const R eps_ht = (d_dw > (R)0 && d_dw < P.mr_R) ? (R)2 * ((R)1 - d_dw * P.mr_inv_R) : (R)0;
@@ -538,16 +597,14 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
         Z_HT = rh * P.ht_ZMAX * m_sqrt(ua * ua + va * va + wa_ht * wa_ht) * wa_ht;
     else
         Z_HT = rh * (P.ht_ZUU * aua * ua + P.ht_ZUW * aua * wa_ht);
-
-    // ---- vertical tail (:347-361)
+    // ---- vertical tail
     const R va_vt = va + vi_tr - P.vt_D * r;
     R Y_VT;
     if (m_fabs(va_vt) > (R)0.3 * aua)
         Y_VT = rh * P.vt_YMAX * m_sqrt(ua * ua + va_vt * va_vt) * va_vt;
     else
         Y_VT = rh * (P.vt_YUU * aua * ua + P.vt_YUV * aua * va_vt);
-
-    // ---- wing (:363-383); the AW109 has none (ZUW = 0), the branch is uniform
+    // ---- wing; the AW109 has none (ZUW = 0), the branch is uniform
     R X_WN = (R)0, Z_WN = (R)0;
     if (P.wn_on) {
         const R wa_w = wa - vi_mr;
@@ -557,12 +614,9 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
         X_WN = -rh * (R)(1.0 / kPi) * m_rcp(vta2) * qq * qq;
     }
     const R power_wn = m_fabs(X_WN * ua);
-
-    // ---- landing gear (:385-398).  QUIRK: the moment uses the ACCUMULATED force (:397).
-    // z + h is formed with the cancellation first (Ground::zh), so the stiff spring force
-    // K * (pos_z + h) keeps its precision near the ground.
+    // ---- landing gear.  QUIRK: the moment uses the ACCUMULATED force (:397).
     R Fl0 = 0, Fl1 = 0, Fl2 = 0, Ml0 = 0, Ml1 = 0, Ml2 = 0;
-    const R zh = gc.zh(z);
+    const R zh = f.zh, B02 = f.B02, B12 = f.B12, B22 = f.B22;
     // Contact is rare.  A gear point's pos_z + h is zh + (B^T r_g)_z <= zh + |r_g|, so no point can
     // touch while zh + max|r_g| <= -WL_CG/12 (lg_reach carries a rounding margin): the wave skips
     // the per-point tests and the spring-damper code unless one of its lanes is that close.
@@ -573,7 +627,7 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
         const R pzh = zh + (B02 * rx + B12 * ry + B22 * rz);   // pos_z + h
         if (-pzh - P.wl_cg_ft < (R)0) {                        // -pos_z - (h + WL_CG/12) < 0
             const R cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
-            const R vel_z = n2 + (B02 * cx + B12 * cy + B22 * cz);
+            const R vel_z = f.n2 + (B02 * cx + B12 * cy + B22 * cz);
             const R fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (R)kEps;
             Fl0 += B02 * fz; Fl1 += B12 * fz; Fl2 += B22 * fz;
             Ml0 += ry * Fl2 - rz * Fl1;
@@ -581,15 +635,31 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
             Ml2 += rx * Fl1 - ry * Fl0;
         }
     }
+    o.F[0] = X_WN + Fl0;
+    o.F[1] = thr_t + Y_VT + Fl1;
+    o.F[2] = Z_HT + Z_WN + Fl2;
+    o.M[0] = thr_t * P.tr_H + Y_VT * P.vt_H + Ml0;
+    o.M[1] = Z_HT * P.ht_D + Ml1;
+    o.M[2] = Ml2 - thr_t * P.tr_D - Y_VT * P.vt_D;
+    o.power = power_tr + power_wn;
+    return o;
+}
 
-    // ---- totals and rigid-body EOM (:446-470)
-    const R p_extra = power_climb + power_fus;
-    const R Fx = X_MR + X_F + X_WN + P.wt * B02 + Fl0;
-    const R Fy = Y_MR + thr_t + Y_F + Y_VT + P.wt * B12 + Fl1;
-    const R Fz = Z_MR + Z_F + Z_HT + Z_WN + P.wt * B22 + Fl2;
-    const R Mx = L_MR + thr_t * P.tr_H + Y_F * P.fus_H + Y_VT * P.vt_H + Ml0;
-    const R My = M_MR + (Z_F * d_fw - X_F * P.fus_H) + Z_HT * P.ht_D + Ml1;
-    const R Mz = (power_mr * P.mr_inv_OMEGA + p_extra * P.mr_inv_OMEGA) - thr_t * P.tr_D - Y_VT * P.vt_D + Ml2;
+// Totals and the rigid-body equations of motion (:446-470) from the two groups.
+template <typename R>
+HD void eom(const Params<R>& P, const R* __restrict__ s, const Frame<R>& f, const Loads<R>& A, const Loads<R>& B,
+            R* __restrict__ d) {
+    const R uu = s[6], vv = s[7], ww = s[8], p = s[9], q = s[10], r = s[11];
+    d[0] = A.d[0];
+    d[1] = B.d[0];
+    d[2] = P.mr_OMEGA;
+    d[3] = P.tr_OMEGA;
+    d[4] = A.d[1];
+    d[5] = A.d[2];
+    const R Fx = (A.F[0] + B.F[0]) + P.wt * f.B02;
+    const R Fy = (A.F[1] + B.F[1]) + P.wt * f.B12;
+    const R Fz = (A.F[2] + B.F[2]) + P.wt * f.B22;
+    const R Mx = A.M[0] + B.M[0], My = A.M[1] + B.M[1], Mz = A.M[2] + B.M[2];
     d[6] = Fx * P.inv_mass - (q * ww - r * vv);
     d[7] = Fy * P.inv_mass - (r * uu - p * ww);
     d[8] = Fz * P.inv_mass - (p * vv - q * uu);
@@ -600,17 +670,31 @@ HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>&
     d[9] = P.Ji00 * g0 + P.Ji02 * g2;
     d[10] = P.Ji11 * g1;
     d[11] = P.Ji20 * g0 + P.Ji22 * g2;
-    d[12] = phid; d[13] = thd; d[14] = psid;
-    d[15] = n0; d[16] = n1; d[17] = n2;
-    if (OBS) {   // :471-488 (observation at this stage's input state)
-        const R power_total = power_mr + power_tr + p_extra + power_wn + P.p_loss;
-        obs[0] = power_total * (R)(1.0 / 550.0);
-        obs[1] = ua; obs[2] = va; obs[3] = wa;
-        obs[4] = n0; obs[5] = n1; obs[6] = n2;
-        obs[7] = phi; obs[8] = th; obs[9] = psi;
-        obs[10] = p; obs[11] = q; obs[12] = r;
-        obs[13] = s[15]; obs[14] = s[16]; obs[15] = -z; obs[16] = -zh;
-    }
+    d[12] = f.phid; d[13] = f.thd; d[14] = f.psid;
+    d[15] = f.n0; d[16] = f.n1; d[17] = f.n2;
+}
+
+// The observation at this stage's input state (:471-488).
+template <typename R>
+HD void observe(const Params<R>& P, const R* __restrict__ s, const Frame<R>& f, const Loads<R>& A,
+                const Loads<R>& B, R* __restrict__ obs) {
+    obs[0] = ((A.power + B.power) + P.p_loss) * (R)(1.0 / 550.0);
+    obs[1] = f.ua; obs[2] = f.va; obs[3] = f.wa;
+    obs[4] = f.n0; obs[5] = f.n1; obs[6] = f.n2;
+    obs[7] = s[12]; obs[8] = s[13]; obs[9] = s[14];
+    obs[10] = s[9]; obs[11] = s[10]; obs[12] = s[11];
+    obs[13] = s[15]; obs[14] = s[16]; obs[15] = -s[17]; obs[16] = -f.zh;
+}
+
+// One evaluation of the model; with OBS also the 17 observations.
+template <bool OBS, typename R>
+HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>& u, const R W[3],
+                 const Ground<R>& gc, const Attitude<R>& att, R* __restrict__ d, R* __restrict__ obs) {
+    const Frame<R> f = frame(P, s, W, gc, att);
+    const Loads<R> A = main_loads(P, s, u, f);
+    const Loads<R> B = tail_loads(P, s, u, f);
+    eom(P, s, f, A, B, d);
+    if (OBS) observe(P, s, f, A, B, obs);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -731,6 +731,7 @@ def test_specialised_kernel_bitwise_equals_generic(torch, task):
         flags = torch.zeros((N,), dtype=torch.int32, device=env.device)
         for k in range(K):
             env.random_actions(act, seed=9, step=k)
+            act[: N // 2, 0] = -1.0   # low collective on half the envs: crashes and auto-resets
             env.step_async(act, with_reset_info=False)
             rew_sum += torch.nan_to_num(env.reward, nan=0.0)
             flags += env.terminated_u8.int() + 2 * env.truncated_u8.int()
