@@ -178,6 +178,37 @@ __device__ __forceinline__ void store_obs(float* s_obs, const float obs[17], flo
     store_obs_wave<NT>(s_obs + wv * 64 * HG_N_OBS, obs, dst, so, blk0 + wv * 64, n, tid & 63);
 }
 
+// RK4 combinations (dynamics.py:158-171) on pairs of state components, so that they issue as packed
+// fp32 (v_pk_fma_f32: two lanes' worth of fma per instruction at the issue cost of one): each
+// component is rounded exactly as the scalar `acc += 2k; st = hs + k h` / `hs += (acc + k) dt/6`.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <bool FIRST>
+__device__ __forceinline__ void rk_stage(const float* hs, const float* k, float* acc, float* st, float h) {
+#pragma unroll
+    for (int c = 0; c < 18; c += 2) {
+        const f32x2 kk = {k[c], k[c + 1]}, hh = {hs[c], hs[c + 1]};
+        f32x2 aa;
+        if (FIRST) {
+            aa = kk;
+        } else {
+            const f32x2 a0 = {acc[c], acc[c + 1]};
+            aa = a0 + 2.f * kk;
+        }
+        const f32x2 ss = hh + kk * h;
+        acc[c] = aa.x; acc[c + 1] = aa.y;
+        st[c] = ss.x; st[c + 1] = ss.y;
+    }
+}
+
+__device__ __forceinline__ void rk_update(float* hs, const float* k, const float* acc, float dt6) {
+#pragma unroll
+    for (int c = 0; c < 18; c += 2) {
+        const f32x2 kk = {k[c], k[c + 1]}, hh = {hs[c], hs[c + 1]}, aa = {acc[c], acc[c + 1]};
+        const f32x2 r = hh + (aa + kk) * dt6;
+        hs[c] = r.x; hs[c + 1] = r.y;
+    }
+}
+
 // Turbulence noise of a step (wind_dynamics.py:49-52: eta = randn(3) / sqrt(dt)): injected by the
 // caller (ETA), or Box-Muller normals from Philox4x32-10 keyed by (global env id, step, episode).
 template <bool ETA>
@@ -218,17 +249,8 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
         const int w_ = (int)(i >> 6);                                                           \
         if ((tid & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;                      \
     } while (0)
-// two-wave kernel: slot row per wave (block * 2 + role)
-#define PSTAMP(j, ...)                                                                          \
-    do {                                                                                        \
-        asm volatile("" ::__VA_ARGS__);                                                         \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
-        const int w_ = (int)(blockIdx.x * 2 + (tid >> 6));                                      \
-        if (lane == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;                            \
-    } while (0)
 #else
 #define TSTAMP(j, ...) do { } while (0)
-#define PSTAMP(j, ...) do { } while (0)
 #endif
 
 // TASK: reward / success of the task; ETA: noise injected by the caller (else in-kernel Philox);
@@ -321,19 +343,15 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     float e0[3] = {hs[12], hs[13], hs[14]};
     hg::dynamics<false>(P, hs, u, W, h_c, att0, k, obs);
     TSTAMP(5, "v"(k[8]), "v"(k[11]));
-#pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
+    rk_stage<true>(hs, k, acc, st, P.half_dt);
     hg::dynamics<false>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
     TSTAMP(6, "v"(k[8]), "v"(k[11]));
-#pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
+    rk_stage<false>(hs, k, acc, st, P.half_dt);
     hg::dynamics<false>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
     TSTAMP(7, "v"(k[8]), "v"(k[11]));
-#pragma unroll
-    for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.dt; }
+    rk_stage<false>(hs, k, acc, st, P.dt);
     hg::dynamics<true>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
-#pragma unroll
-    for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
+    rk_update(hs, k, acc, P.dt6);
     TSTAMP(8, "v"(hs[8]), "v"(hs[11]), "v"(obs[16]));
     if (FEAT && P.reset_retrim && active && !(P.autoreset_next && step < 0)) {   // F8: a reset trims against this wind
         float* wb = a.retrim_wind + 3 * blk0;
@@ -475,255 +493,6 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     __builtin_amdgcn_s_waitcnt(0);
     TSTAMP(12, "v"(tid));
     if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][14] = __builtin_amdgcn_s_memrealtime();
-#endif
-}
-
-// ------------------------------------------------------------------------------ two-wave step
-// step_kernel's step for launches of at most one wave per SIMD (N <= 64 x 4 x CUs; 65 536 envs on
-// MI355X) with the default airframe's constants compiled in.  At one wave per SIMD the step is
-// bound by that wave's single instruction stream: one wave issues a VALU every ~4-5 cycles while
-// its SIMD can take one every ~2.5 from two waves (MI355X_MICROARCH.md, 'vector-instruction ISSUE
-// cost'; scripts/ubench/issue.hip).  Here every 64 envs get two waves (a 128-thread block), one
-// env per lane in each, and the work of the step is split between them:
-//   * the rotor wave (0) draws the noise and steps the wind; the airframe wave (1) takes the
-//     sines and cosines of the committed attitude;
-//   * every RK stage, both evaluate the kinematics (hg::frame) and the equations of motion
-//     (hg::eom), so both hold the full state, while the rotor wave evaluates the main rotor and
-//     fuselage (hg::main_loads) and the airframe wave the tail rotor, tails, wing and gear
-//     (hg::tail_loads); the two trade their 10 + 10 terms through LDS around one block barrier;
-//   * after the step the rotor wave computes the reward and the airframe wave the post-step ground
-//     height and failure test; the stores are split by column.
-// Same physics.h parts in the same order as step_kernel: the results are bitwise identical
-// (tests/test_gpu_parity.py::test_specialised_kernel_bitwise_equals_generic).
-constexpr int kPairBlock = 128;
-constexpr int kLoadTerms = 10;   // hg::Loads<float>: d[3], F[3], M[3], power
-
-__device__ __forceinline__ void put_loads(float (*x)[64], int l, const hg::Loads<float>& o) {
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        x[j][l] = o.d[j];
-        x[3 + j][l] = o.F[j];
-        x[6 + j][l] = o.M[j];
-    }
-    x[9][l] = o.power;
-}
-
-__device__ __forceinline__ hg::Loads<float> get_loads(const float (*x)[64], int l) {
-    hg::Loads<float> o;
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-        o.d[j] = x[j][l];
-        o.F[j] = x[3 + j][l];
-        o.M[j] = x[6 + j][l];
-    }
-    o.power = x[9][l];
-    return o;
-}
-
-template <int TASK, bool ETA, bool MULTI>
-__global__ __launch_bounds__(kPairBlock, 2) void pair_step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
-                                                                const StepArgs a) {
-    __shared__ float x_main[2][kLoadTerms][64];   // rotor wave -> airframe wave, by RK-stage parity
-    __shared__ float x_tail[2][kLoadTerms][64];   // airframe wave -> rotor wave
-    __shared__ float x_wind[3][64];               // wind of the step (rotor -> airframe)
-    __shared__ float x_att[6][64];                // sin / cos of the committed attitude (airframe -> rotor)
-    __shared__ int32_t x_flag[2][64];             // success_step (rotor), failed (airframe)
-    __shared__ float s_obs[64 * HG_N_OBS];        // airframe wave's observation staging
-    Params<float> P = *Pa;
-    hg::bake(P);
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const bool rotor = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;   // wave-uniform role
-    const int64_t blk0 = (int64_t)blockIdx.x * 64;
-    const int64_t i = blk0 + lane;
-    const int64_t n = a.n;
-    const bool active = i < n;
-    const uint32_t lo = (uint32_t)(active ? lane : 0);
-    float* st_b = a.state + blk0;
-    int32_t* ct_b = a.counters + blk0;
-#if HG_TIMING
-    if (lane == 0 && blockIdx.x * 2 + (tid >> 6) < HG_TIMING_WAVES)
-        g_timing[blockIdx.x * 2 + (tid >> 6)][15] = __builtin_amdgcn_s_memrealtime();
-#endif
-    PSTAMP(0, "v"(tid));
-
-    float hs[18], ws[5], carry[4];
-    hs[15] = ld_lane(COL(st_b, 15), lo);
-    hs[16] = ld_lane(COL(st_b, 16), lo);
-    int32_t step = ld_lane(COL(ct_b, 0), lo), succ = ld_lane(COL(ct_b, 1), lo), epi = ld_lane(COL(ct_b, 2), lo);
-    if (rotor) {
-#pragma unroll
-        for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lo);
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lo);
-#pragma unroll
-    for (int c = 0; c < 18; ++c)
-        if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lo);
-    const int nsteps = MULTI ? a.nsteps : 1;
-    for (int sstep = 0; sstep < nsteps; ++sstep) {
-        const int64_t so = MULTI ? (int64_t)sstep * n : 0;
-        const float4 act = ld_lane(reinterpret_cast<const float4*>(a.actions) + so + blk0, lo);
-        const hg::GroundCell<float> cell_c = hg::ground_cell(P, hs[15], hs[16]);
-        const hg::GroundTexels tex_c = hg::ground_fetch(a.hmap, cell_c);
-        PSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(carry[3]));
-        float W[3];
-        hg::Attitude<float> att0;
-        if (rotor) {   // noise and wind step (Heli.step :195-199)
-            float eta[3];
-            draw_eta<ETA>(a, P, so, blk0, lo, step, epi, eta);
-            hg::wind_step(P, ws, carry, eta, W);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) x_wind[j][lane] = W[j];
-        } else {
-            att0 = hg::attitude(hs + 12);
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                x_att[j][lane] = att0.s[j];
-                x_att[3 + j][lane] = att0.c[j];
-            }
-        }
-        PSTAMP(2, "v"(tid));
-        __syncthreads();
-        PSTAMP(3, "v"(tid));
-        if (rotor) {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                att0.s[j] = x_att[j][lane];
-                att0.c[j] = x_att[3 + j][lane];
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 3; ++j) W[j] = x_wind[j][lane];
-        }
-        const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
-
-        // RK4 (dynamics.py:158-171) with the loads of each stage split over the two waves
-        const hg::Controls<float> u = hg::controls(P, act.x, act.y, act.z, act.w);
-        float k[18], acc[18], st[18], obs[17];
-        const float e0[3] = {hs[12], hs[13], hs[14]};
-#pragma unroll
-        for (int stg = 0; stg < 4; ++stg) {
-            const float* si = stg == 0 ? hs : st;
-            const hg::Attitude<float> att = stg == 0 ? att0 : hg::attitude_step(att0, e0, st + 12);
-            const hg::Frame<float> f = hg::frame(P, si, W, h_c, att);
-            hg::Loads<float> A, B;
-            if (rotor) {
-                A = hg::main_loads(P, si, u, f);
-                put_loads(x_main[stg & 1], lane, A);
-            } else {
-                B = hg::tail_loads(P, si, u, f);
-                put_loads(x_tail[stg & 1], lane, B);
-            }
-            PSTAMP(4 + 2 * stg, "v"(tid));
-            __syncthreads();
-            PSTAMP(5 + 2 * stg, "v"(tid));
-            if (rotor) B = get_loads(x_tail[stg & 1], lane);
-            else A = get_loads(x_main[stg & 1], lane);
-            hg::eom(P, si, f, A, B, k);
-            if (stg == 3) hg::observe(P, si, f, A, B, obs);
-            if (stg == 0) {
-#pragma unroll
-                for (int c = 0; c < 18; ++c) { acc[c] = k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
-            } else if (stg == 1) {
-#pragma unroll
-                for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.half_dt; }
-            } else if (stg == 2) {
-#pragma unroll
-                for (int c = 0; c < 18; ++c) { acc[c] += 2.f * k[c]; st[c] = hs[c] + k[c] * P.dt; }
-            } else {
-#pragma unroll
-                for (int c = 0; c < 18; ++c) hs[c] = hs[c] + (acc[c] + k[c]) * P.dt6;
-            }
-        }
-        const float tpl = lane < kTplFloats ? reinterpret_cast<const float*>(Tp)[lane] : 0.f;
-        // step_after (helicopter_dynamics.py:73-77)
-        hs[2] = hg::pi_bound(hs[2]);
-        hs[3] = hg::pi_bound(hs[3]);
-        hs[4] = hg::pi_bound(hs[4]);
-        hs[5] = hg::pi_bound(hs[5]);
-        hs[12] = hg::pi_bound(hs[12]);
-        hs[13] = hg::pi_bound(hs[13]);
-        hs[14] = hg::pi_bound(hs[14]);
-
-        // reward (rotor wave) and failure test (airframe wave), exchanged
-        bool success_step = false, failed = false;
-        float rew = 0.f;
-        if (rotor) {
-            if (TASK == HG_TASK_HOVER) rew = hg::reward_hover(P, hs, k, &success_step);
-            if (TASK == HG_TASK_FORWARD_FLIGHT) rew = hg::reward_forward(P, hs, k, &success_step);
-            x_flag[0][lane] = success_step ? 1 : 0;
-        } else {
-            const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
-            failed = hg::is_failed(P, hs, k, h_post);
-            x_flag[1][lane] = failed ? 1 : 0;
-        }
-        PSTAMP(12, "v"(hs[0]), "v"(rew));
-        __syncthreads();
-        if (rotor) failed = x_flag[1][lane] != 0;
-        else success_step = x_flag[0][lane] != 0;
-        step += 1;
-        const bool successed = succ >= P.success_steps;   // successed_time before this step's add
-        const bool time_up = step >= P.time_up_steps;
-        const bool term = failed || successed;
-        const bool trunc = time_up;
-        const bool done = term || trunc;
-        succ += success_step ? 1 : 0;
-        const bool do_reset = P.autoreset && active && done;
-        if (rotor) {
-            if (active) st_lane<true>(a.reward + so + blk0, (uint32_t)lane, rew);
-        } else if (active) {
-            st_lane<true>(a.terminated + so + blk0, (uint32_t)lane, (uint8_t)term);
-            st_lane<true>(a.truncated + so + blk0, (uint32_t)lane, (uint8_t)trunc);
-            if (a.info)
-                st_lane<true>(a.info + so + blk0, (uint32_t)lane,
-                              (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
-                                        (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0)));
-        }
-        // same-step auto-reset from the template, float c held by lane c (heli 18 | carry 4 | obs 17)
-        if (do_reset) {
-#pragma unroll
-            for (int c = 0; c < 18; ++c) hs[c] = lane_value(tpl, c);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) carry[c] = lane_value(tpl, 18 + c);
-#pragma unroll
-            for (int c = 0; c < 17; ++c) obs[c] = lane_value(tpl, 22 + c);
-#pragma unroll
-            for (int c = 0; c < 5; ++c) ws[c] = 0.f;
-            step = 0;
-            succ = 0;
-            epi += 1;
-        } else {
-            carry[0] = obs[4];
-            carry[1] = obs[5];
-            carry[2] = obs[6];
-            carry[3] = obs[16];
-        }
-        if (!rotor) store_obs_wave<true>(s_obs, obs, a.obs, so, blk0, n, lane);
-    }   // steps
-    // state: heli + wind by the rotor wave, carry + counters by the airframe wave
-    st_b = a.state + blk0;
-    ct_b = a.counters + blk0;
-    asm volatile("" : "+s"(st_b), "+s"(ct_b));
-    if (active) {
-        if (rotor) {
-#pragma unroll
-            for (int c = 0; c < 18; ++c) st_lane<true>(COL(st_b, c), (uint32_t)lane, hs[c]);
-#pragma unroll
-            for (int c = 0; c < 5; ++c) st_lane<true>(COL(st_b, 18 + c), (uint32_t)lane, ws[c]);
-        } else {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) st_lane<true>(COL(st_b, 23 + c), (uint32_t)lane, carry[c]);
-            st_lane<true>(COL(ct_b, 0), (uint32_t)lane, step);
-            st_lane<true>(COL(ct_b, 1), (uint32_t)lane, succ);
-            st_lane<true>(COL(ct_b, 2), (uint32_t)lane, epi);
-        }
-    }
-#if HG_TIMING
-    __builtin_amdgcn_s_waitcnt(0);
-    PSTAMP(13, "v"(tid));
-    if (lane == 0 && blockIdx.x * 2 + (tid >> 6) < HG_TIMING_WAVES)
-        g_timing[blockIdx.x * 2 + (tid >> 6)][14] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
@@ -1134,21 +903,10 @@ static inline unsigned retrim_grid(int64_t jobs) {
 
 #define PARAM_ARG(e) ((const Params<float>*)(e)->params_dev)
 
-// The default airframe's constant-specialised step for launches of at most one wave per SIMD:
-// the two-wave kernel (HG_PAIR, default), or step_kernel<..., BAKED> (diagnostic builds, A/B).
-#ifndef HG_PAIR
-#define HG_PAIR 1
-#endif
-static inline unsigned pair_grid(int64_t n) { return (unsigned)((n + 63) / 64); }
-#if HG_PAIR
-#define HG_LAUNCH_SPECIALISED(T, ETA_, MULTI_)                                                             \
-    hipLaunchKernelGGL((pair_step_kernel<T, ETA_, MULTI_>), dim3(pair_grid(e->n)), dim3(kPairBlock), 0, s, \
-                       PARAM_ARG(e), e->tmpl_dev, a)
-#else
-#define HG_LAUNCH_SPECIALISED(T, ETA_, MULTI_)                                                             \
-    hipLaunchKernelGGL((step_kernel<T, ETA_, true, false, MULTI_, true>), grid, block, 0, s, PARAM_ARG(e), \
+// The default airframe's constant-specialised step (baked.h).
+#define HG_LAUNCH_SPECIALISED(T, ETA_, NT_, MULTI_)                                                        \
+    hipLaunchKernelGGL((step_kernel<T, ETA_, NT_, false, MULTI_, true>), grid, block, 0, s, PARAM_ARG(e),  \
                        e->tmpl_dev, a)
-#endif
 
 extern "C" {
 #if HG_TIMING
@@ -1427,9 +1185,9 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
         if (feat) {                                                                                              \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
-        } else if (NT && e->baked) {                                                                             \
-            if (eta) HG_LAUNCH_SPECIALISED(T, true, false);                                                      \
-            else HG_LAUNCH_SPECIALISED(T, false, false);                                                         \
+        } else if (e->baked) {                                                                                   \
+            if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, false);                                                  \
+            else HG_LAUNCH_SPECIALISED(T, false, NT, false);                                                     \
         } else {                                                                                                 \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
@@ -1501,9 +1259,9 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
         if (feat) {                                                                                              \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
-        } else if (NT && e->baked) {                                                                             \
-            if (eta) HG_LAUNCH_SPECIALISED(T, true, true);                                                       \
-            else HG_LAUNCH_SPECIALISED(T, false, true);                                                          \
+        } else if (e->baked) {                                                                                   \
+            if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, true);                                                   \
+            else HG_LAUNCH_SPECIALISED(T, false, NT, true);                                                      \
         } else {                                                                                                 \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \

@@ -17,37 +17,11 @@ PHASES = ["state loads", "philox", "wind step", "ground h_c", "RK stage 1", "RK 
 ORDER = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 11, 12]   # stamp slots in program order
 
 
-# two-wave kernel (pair_step_kernel): rows = block * 2 + role (0 rotor wave, 1 airframe wave)
-PAIR_PHASES = ["state loads", "noise+wind | attitude", "pre-stage barrier wait", "stage 1 loads",
-               "stage 1 barrier wait", "stage 2 (eom+frame+loads)", "stage 2 barrier wait",
-               "stage 3 (eom+frame+loads)", "stage 3 barrier wait", "stage 4 (eom+frame+loads)",
-               "stage 4 barrier wait", "eom/update/wraps/reward|failed", "flag barrier + stores + drain"]
-
-
-def pair_report(buf, nw):
-    t = buf[:nw, :14].astype(np.int64)
-    rt = buf[:nw, 14:16].astype(np.int64)
-    span_cyc = (t[:, 13] - t[:, 0]).astype(np.float64)
-    span_ns = (rt[:, 0] - rt[:, 1]) * 10.0
-    ghz = np.median(span_cyc / np.maximum(span_ns, 1))
-    starts = (rt[:, 1] - rt[:, 1].min()) * 10.0
-    ends = (rt[:, 0] - rt[:, 1].min()) * 10.0
-    print(f"waves {nw}; clock ~{ghz:.2f} GHz; wave life median {np.median(span_ns)/1e3:.2f} us; "
-          f"start spread p90 {np.percentile(starts, 90)/1e3:.2f} us; last wave end {ends.max()/1e3:.2f} us")
-    d = np.diff(t, axis=1).astype(np.float64) / ghz / 1e3
-    for role, name in ((0, "rotor"), (1, "airframe")):
-        dr = d[role::2]
-        print(f" {name} wave:")
-        for j, ph in enumerate(PAIR_PHASES):
-            print(f"  {ph:34s} median {np.median(dr[:, j]):6.3f} us   p90 {np.percentile(dr[:, j], 90):6.3f} us")
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--warm", type=int, default=300)
     ap.add_argument("--dt", type=float, default=0.01)
-    ap.add_argument("--pair", action="store_true", help="the library runs the two-wave kernel")
     args = ap.parse_args()
     import torch
     from heligym_amd import HeliVecEnv
@@ -62,10 +36,6 @@ def main():
     fn = env.lib.hg_debug_timing
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     assert fn(buf.ctypes.data, buf.nbytes) == 0
-    if args.pair:
-        pair_report(buf, min(2048, 2 * ((args.envs + 63) // 64)))
-        env.close()
-        return
     nw = min(2048, args.envs // 64)
     t = buf[:nw, ORDER].astype(np.int64)
     rt = buf[:nw, 14:16].astype(np.int64)        # [end, start] s_memrealtime (100 MHz)
