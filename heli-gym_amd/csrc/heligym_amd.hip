@@ -111,9 +111,6 @@ using ParamArg = const Params<float>* __restrict__;
 #ifndef HG_MIN_WAVES_BULK   // launches with more waves than SIMDs (not NT)
 #define HG_MIN_WAVES_BULK 1
 #endif
-#ifndef HG_PREDICT_CELL
-#define HG_PREDICT_CELL 0
-#endif
 
 constexpr int kTplFloats = (int)(sizeof(Template<float>) / sizeof(float));
 static_assert(kTplFloats <= 64, "reset template must fit one float per lane");
@@ -315,13 +312,6 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     // terrain texels under the committed position (F6): issued now, combined after the wind step
     const hg::GroundCell<float> cell_c = hg::ground_cell(P, hs[15], hs[16]);
     const hg::GroundTexels tex_c = hg::ground_fetch(a.hmap, cell_c);
-#if HG_PREDICT_CELL
-    // texels of the cell the env is predicted to end the step in (position + dt * last velocity):
-    // issued now, so the post-step ground height needs no dependent fetch unless the prediction
-    // misses (the env crosses a cell edge it was not heading for)
-    const hg::GroundCell<float> cell_p = hg::ground_cell(P, hs[15] + P.dt * carry[0], hs[16] + P.dt * carry[1]);
-    const hg::GroundTexels tex_p = hg::ground_fetch(a.hmap, cell_p);
-#endif
 
     TSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(epi), "v"(carry[3]), "v"(ws[4]));
     // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
@@ -378,16 +368,7 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     float rew = 0.f;
     if (TASK == HG_TASK_HOVER) rew = hg::reward_hover(P, hs, k, &success_step);
     if (TASK == HG_TASK_FORWARD_FLIGHT) rew = hg::reward_forward(P, hs, k, &success_step);
-#if HG_PREDICT_CELL
-    const hg::GroundCell<float> cell_q = hg::ground_cell(P, hs[15], hs[16]);
-    hg::GroundTexels tex_q = tex_p;
-    const bool cell_miss = cell_q.mid != cell_p.mid;
-    if (hg::wave_any(cell_miss))
-        if (cell_miss) tex_q = hg::ground_fetch(a.hmap, cell_q);
-    const hg::Ground<float> h_post = hg::ground_combine<float>(tex_q, cell_q);
-#else
     const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
-#endif
     step += 1;
     const bool failed = hg::is_failed(P, hs, k, h_post);
     TSTAMP(10, "v"(rew), "v"((int)failed));

@@ -8,10 +8,10 @@ import re
 import shutil
 import sys
 
-# step_kernel<TASK, ETA, NT, FEAT, MULTI>: the per-step launch (MULTI false) is the judged kernel;
-# hg_rollout's multi-step launches (MULTI true) are summarised separately.
-SINGLE = re.compile(r"step_kernel<\d+(, (true|false)){2,3}(, false)?>")
-MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true>")
+# step_kernel<TASK, ETA, NT, FEAT, MULTI, BAKED>: the per-step launch (MULTI false) is the judged
+# kernel; hg_rollout's multi-step launches (MULTI true) are summarised separately.
+SINGLE = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, (true|false)>")
+MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true, (true|false)>")
 
 d, tag, n, dt = sys.argv[1], sys.argv[2], int(sys.argv[3]), float(sys.argv[4])
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
