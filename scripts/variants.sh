@@ -3,7 +3,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 out=gpurun_out/variants.jsonl; : > $out
 for v in ${VARIANTS:-A B C D}; do
-  for n in 65536 1048576; do
+  for n in ${SIZES:-65536 1048576}; do
     HELIGYM_AMD_LIB=$PWD/build/variants/$v.so timeout -k 10 200 python bench.py --envs $n --steps 1000 --no-cpu-baseline \
       | python -c "import sys,json; d=json.loads(sys.stdin.read()); d['variant']='$v'; print(json.dumps(d))" >> $out \
       || { echo "variant $v failed"; exit 3; }
