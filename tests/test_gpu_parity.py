@@ -715,12 +715,14 @@ def test_per_env_trim_conditions(torch):
     env.close()
 
 
-@pytest.mark.parametrize("task", ["hover", "forward_flight"])
-def test_specialised_kernel_bitwise_equals_generic(torch, task):
+@pytest.mark.parametrize("task,N,K", [("hover", 4096, 300), ("forward_flight", 4096, 300),
+                                      ("hover", 300_000, 300)])   # the last: more waves than SIMDs
+def test_specialised_kernel_bitwise_equals_generic(torch, task, N, K):
     """The default airframe's constant-specialised kernel (csrc/baked.h: the model constants as
     instruction literals) and the generic kernel (constants loaded from the device copy) give
-    bitwise-identical steps and rollouts: random actions, in-kernel turbulence, auto-resets."""
-    N, K, R = 4096, 300, 50
+    bitwise-identical steps and rollouts: random actions, in-kernel turbulence, auto-resets; for a
+    batch within one wave per SIMD (non-temporal store path) and one past it."""
+    R = 50
 
     def run(spec):
         env = make_env(torch, N, task, 0.01, autoreset=True, seed=3)
