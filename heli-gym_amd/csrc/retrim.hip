@@ -12,6 +12,22 @@
 namespace hgk {
 namespace {
 
+#ifndef HG_TIMING
+#define HG_TIMING 0
+#endif
+#if HG_TIMING
+// diagnostic build: s_memtime at the phase boundaries of the first job's rounds (lane 0)
+__device__ unsigned long long g_rt_timing[64];
+#define RSTAMP(j, ...)                                                                \
+    do {                                                                              \
+        asm volatile("" ::__VA_ARGS__);                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                   \
+        if (l == 0 && job == 0 && (j) < 64) g_rt_timing[(j)] = t_;                    \
+    } while (0)
+#else
+#define RSTAMP(j, ...) do { } while (0)
+#endif
+
 // HelicopterDynamics.trim (helicopter_dynamics.py:491-555) for many winds at once: the reset path of
 // reset_mode RETRIM (F8) and hg_trim_batch.  One wave per trim, fp64 throughout, every lane holding
 // the same Newton iterate:
@@ -33,6 +49,68 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     const uint32_t lo = __shfl((int)(uint32_t)u, src);
     const uint32_t hi = __shfl((int)(uint32_t)(u >> 32), src);
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// hg::solve16 (np.linalg.inv(dydx) @ r, helicopter_dynamics.py:524-527) on the augmented matrix
+// [J | r] (16 x 17 doubles, row-major) in LDS: Gauss-Jordan with partial pivoting in the host
+// solver's operation order.  Every lane reads the pivot column (broadcast reads) and finds the
+// pivot itself; lane e owns the elements e, e + 64, ... of the elimination, whose operands (the
+// row's multiplier and the pivot row's element) are all read before any element is written.
+constexpr int kGJElems = 16 * 17;
+
+// The block is one wave, whose LDS operations execute in issue order: a read issued after a write
+// sees it.  This only keeps the compiler from reordering LDS accesses across the point (no
+// s_barrier, no wait for the LDS queue to drain).
+__device__ __forceinline__ void lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+constexpr int kGJPerLane = (kGJElems + 63) / 64;
+
+__device__ __forceinline__ bool gauss_jordan(double* M, int l) {
+    int ei[kGJPerLane], ej[kGJPerLane];   // row / column of this lane's elements
+#pragma unroll
+    for (int k = 0; k < kGJPerLane; ++k) {
+        ei[k] = (l + 64 * k) / 17;
+        ej[k] = (l + 64 * k) - 17 * ei[k];
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        int p = c;   // first row of maximal |M[i][c]| among rows c..15 (strict >, as the host)
+        double mp = M[c * 17 + c];
+#pragma unroll
+        for (int i = c + 1; i < 16; ++i) {
+            const double v = M[i * 17 + c];
+            if (fabs(v) > fabs(mp)) { p = i; mp = v; }
+        }
+        if (mp == 0.0 || !isfinite(mp)) return false;
+        if (p != c) {   // wave-uniform
+            lds_order();
+            if (l < 17) {
+                const double t = M[c * 17 + l];
+                M[c * 17 + l] = M[p * 17 + l];
+                M[p * 17 + l] = t;
+            }
+        }
+        lds_order();
+        if (l >= c && l < 17) M[c * 17 + l] /= mp;   // the pivot row, j >= c
+        lds_order();
+        double f[kGJPerLane], pr[kGJPerLane];
+#pragma unroll
+        for (int k = 0; k < kGJPerLane; ++k) {
+            const bool in = l + 64 * k < kGJElems;
+            f[k] = in ? M[ei[k] * 17 + c] : 0.0;
+            pr[k] = in ? M[c * 17 + ej[k]] : 0.0;
+        }
+        lds_order();
+#pragma unroll
+        for (int k = 0; k < kGJPerLane; ++k) {
+            const int e = l + 64 * k;
+            if (e < kGJElems && ei[k] != c && ej[k] >= c && f[k] != 0.0) M[e] -= f[k] * pr[k];
+        }
+        lds_order();
+    }
+    return true;
 }
 
 __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, int64_t env, const double x[16],
@@ -60,6 +138,7 @@ __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, i
 // alone the residual at x0 in the first round.  A round is one trim_fcn latency; a trim of three
 // Newton steps takes four rounds.
 __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
+    __shared__ double M[kGJElems];   // [J | r] of the current Newton step
     const int l = threadIdx.x;
     const hg::Params<double>& P = *a.P;
     const double eps = hg::kTrimEps;
@@ -79,6 +158,8 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
         double tol = 0;
         int it = 0;
         bool ok = true, done = false, first = true, have_jac = false;
+        int round = 0;
+        RSTAMP(0, "v"(l));
         while (!done) {
             // ---- one evaluation round
             const int c = l & 15;
@@ -94,8 +175,10 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
                 for (int k = 0; k < 16; ++k) xe[k] = first ? x[k] : x[k] - step * dir[k];
             }
             double ye[16], se[18], de[18], oe[17];
+            RSTAMP(1 + 4 * round, "v"(xe[0]));
             hg::trim_fcn(P, T.base, xe, W, T.hc, ye, se, de, oe);
             const double te = hg::trim_residual(ye, T.yt);
+            RSTAMP(2 + 4 * round, "v"(te));
             // ---- accept a trial (or take the base point)
             int src = 32;   // lane whose evaluation is the new iterate
             if (first) {
@@ -132,48 +215,23 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
                     hg::trim_fcn(P, T.base, xe, W, T.hc, ye, nullptr, nullptr, nullptr);
                 }
             }
-            // ---- Newton direction: Gauss-Jordan (hg::solve16), lane j <= 16 owns column j of [J | r]
-            double col[16];
+            // ---- Newton direction: [J | r] into LDS (lane j <= 16 holds column j), then Gauss-Jordan
             for (int k = 0; k < 16; ++k) {
                 const double ym = shfl_d(ye[k], (l + 16) & 63);
-                col[k] = l < 16 ? (ye[k] - ym) / (2 * eps) : y[k] - T.yt[k];
+                const double v = l < 16 ? (ye[k] - ym) / (2 * eps) : y[k] - T.yt[k];
+                if (l < 17) M[k * 17 + l] = v;
             }
-#pragma unroll
-            for (int cc = 0; cc < 16; ++cc) {
-                double bc[16];   // column cc, broadcast to every lane
-#pragma unroll
-                for (int k = 0; k < 16; ++k) bc[k] = read_lane(col[k], cc);
-                int p = cc;
-#pragma unroll
-                for (int i = cc + 1; i < 16; ++i)
-                    if (fabs(bc[i]) > fabs(bc[p])) p = i;
-                p = __builtin_amdgcn_readfirstlane(p);
-                double mp = bc[cc];
-#pragma unroll
-                for (int i = cc + 1; i < 16; ++i)
-                    if (i == p) mp = bc[i];
-                if (mp == 0.0 || !isfinite(mp)) { ok = false; break; }
-                if (p != cc) {
-#pragma unroll
-                    for (int i = cc + 1; i < 16; ++i)
-                        if (i == p) {
-                            double t = col[cc]; col[cc] = col[i]; col[i] = t;
-                            t = bc[cc]; bc[cc] = bc[i]; bc[i] = t;
-                        }
-                }
-                const double piv = bc[cc];
-                if (l >= cc) col[cc] /= piv;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    if (i == cc) continue;
-                    const double f = bc[i];
-                    if (l >= cc && f != 0.0) col[i] -= f * col[cc];
-                }
-            }
+            __syncthreads();
+            RSTAMP(3 + 4 * round, "v"(ye[0]));
+            ok = gauss_jordan(M, l);
             if (!ok) break;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) dir[k] = read_lane(col[k], 16);
+            for (int k = 0; k < 16; ++k) dir[k] = M[k * 17 + 16];
+            __syncthreads();   // dir read before the next round's matrix is written
+            RSTAMP(4 + 4 * round, "v"(dir[0]));
+            ++round;
         }
+        RSTAMP(63, "v"(l));
         if (ok && done && l == 0) {
             // the search stopped without converging (:540): final evaluation at the kept x
             bool written = !(tol > eps);
@@ -192,6 +250,12 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
 
 
 }  // namespace
+
+#if HG_TIMING
+extern "C" int hg_debug_retrim_timing(void* dst, int64_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rt_timing), (size_t)bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t launch_retrim(const RetrimArgs& a, unsigned grid, hipStream_t stream) {
     hipLaunchKernelGGL(retrim_kernel, dim3(grid), dim3(64), 0, stream, a);
