@@ -254,8 +254,9 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
 // NT: streaming output stores (see st_out); FEAT: the optional features (reset-info compaction,
 // per-reset re-trim, next-step auto-reset, TimeLimit) -- without them the kernel carries none of
 // their registers; MULTI: a.nsteps consecutive steps per launch (hg_rollout) with the env state
-// kept in registers between them.  All compile-time, so the hot kernel has no data-independent
-// branches to merge around.
+// kept in registers between them; BAKED: the default airframe's model constants compiled in as
+// instruction literals (baked.h), the runtime fields still read from the device copy.  All
+// compile-time, so the hot kernel has no data-independent branches to merge around.
 template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
 __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
