@@ -221,6 +221,33 @@ def main():
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
     elapsed = float(el_t[0])
 
+    # Secondary figure (not `value`): the same step with the generic kernel (model constants loaded
+    # from the device copy, as for any non-default airframe); bitwise-identical results.
+    generic = None
+    if env.specialized and gathered is None and not args.generic_kernel:
+        env.set_specialized(False)
+        gg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gg):
+            for k in range(B):
+                one_step(k)
+        gg.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0.record()
+        for _ in range(reps):
+            gg.replay()
+        g1.record()
+        torch.cuda.synchronize()
+        gt = torch.tensor([g0.elapsed_time(g1) * 1e-3], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        generic = {"kernel": "generic (constants loaded, any airframe)", "value": N * world * K / float(gt[0]),
+                   "unit": "env-steps/s", "ms_per_step": float(gt[0]) / K * 1e3}
+        env.set_specialized(True)
+        del gg
+
     # Secondary figure (not `value`): the same workload as open-loop rollouts, hg_rollout over the
     # same action bank, `rollout_steps` steps per launch with the env state kept in registers.
     roll = None
@@ -291,6 +318,8 @@ def main():
                      "algorithmic_bytes_per_launch": N * BYTES_PER_ENV_STEP},
         "wall_s": float(el_t[1]),
     }
+    if generic is not None:
+        out["generic_kernel"] = generic
     if roll is not None:
         out["rollout"] = roll
     tr = pmc_traffic(N, args.dt, args.task)
