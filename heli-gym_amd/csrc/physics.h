@@ -461,6 +461,14 @@ HD void wind_step(const Params<R>& P, R s[5], const R carry[4], const R eta[3],
 // height under the COMMITTED position (F6).
 
 // Stage-input kinematics (:423-445, kinematic.py:3-29, ISA density :160-165).
+// A pair of R as a vector (packed fp32 on the device for R = float).
+template <typename R>
+struct V2T {
+    typedef R type __attribute__((ext_vector_type(2)));
+};
+template <typename R>
+using V2 = typename V2T<R>::type;
+
 template <typename R>
 struct Frame {
     R B02, B12, B22;     // third column of the earth->body DCM (gravity, landing gear)
@@ -475,28 +483,57 @@ template <typename R>
 HD Frame<R> frame(const Params<R>& P, const R* __restrict__ s, const R W[3], const Ground<R>& gc,
                   const Attitude<R>& att) {
     const R uu = s[6], vv = s[7], ww = s[8], p = s[9], q = s[10], r = s[11];
-    // kinematic.py:3-29: B = earth->body DCM, T = pqr->euler rate
     const R s0 = att.s[0], c0 = att.c[0], s1 = att.s[1], c1 = att.c[1], s2 = att.s[2], c2 = att.c[2];
-    const R B00 = c1 * c2, B01 = c1 * s2, B02 = -s1;
-    const R s0s1 = s0 * s1, c0s1 = c0 * s1;
-    const R B10 = s0s1 * c2 - c0 * s2, B11 = s0s1 * s2 + c0 * c2, B12 = s0 * c1;
-    const R B20 = c0s1 * c2 + s0 * s2, B21 = c0s1 * s2 - s0 * c2, B22 = c0 * c1;
+    Frame<R> f;
+    // euler rates T(phi, theta) pqr (kinematic.py:20-29)
     const R ic1 = m_rcp(c1);
     const R t1 = s1 * ic1;
-    Frame<R> f;
-    f.B02 = B02;
-    f.B12 = B12;
-    f.B22 = B22;
-    f.phid = p + (s0 * t1) * q + (c0 * t1) * r;
-    f.thd = c0 * q - s0 * r;
-    f.psid = (s0 * ic1) * q + (c0 * ic1) * r;
-    // ned = B^T uvw, uvw_air = uvw - B W (:428-431)
-    f.n0 = B00 * uu + B10 * vv + B20 * ww;
-    f.n1 = B01 * uu + B11 * vv + B21 * ww;
-    f.n2 = B02 * uu + B12 * vv + B22 * ww;
-    f.ua = uu - (B00 * W[0] + B01 * W[1] + B02 * W[2]);
-    f.va = vv - (B10 * W[0] + B11 * W[1] + B12 * W[2]);
-    f.wa = ww - (B20 * W[0] + B21 * W[1] + B22 * W[2]);
+    if constexpr (sizeof(R) == sizeof(double)) {
+        // fp64 (the trims): the reference's form, B = Rx Ry Rz formed as a matrix (kinematic.py:3-17)
+        // and applied to uvw and W (:428-431).  The trim's Newton path is sensitive to the operation
+        // order at ill-conditioned points, so it follows the reference's as closely as possible.
+        const R B00 = c1 * c2, B01 = c1 * s2, B02 = -s1;
+        const R s0s1 = s0 * s1, c0s1 = c0 * s1;
+        const R B10 = s0s1 * c2 - c0 * s2, B11 = s0s1 * s2 + c0 * c2, B12 = s0 * c1;
+        const R B20 = c0s1 * c2 + s0 * s2, B21 = c0s1 * s2 - s0 * c2, B22 = c0 * c1;
+        f.B02 = B02;
+        f.B12 = B12;
+        f.B22 = B22;
+        f.phid = p + (s0 * t1) * q + (c0 * t1) * r;
+        f.thd = c0 * q - s0 * r;
+        f.psid = (s0 * ic1) * q + (c0 * ic1) * r;
+        f.n0 = B00 * uu + B10 * vv + B20 * ww;
+        f.n1 = B01 * uu + B11 * vv + B21 * ww;
+        f.n2 = B02 * uu + B12 * vv + B22 * ww;
+        f.ua = uu - (B00 * W[0] + B01 * W[1] + B02 * W[2]);
+        f.va = vv - (B10 * W[0] + B11 * W[1] + B12 * W[2]);
+        f.wa = ww - (B20 * W[0] + B21 * W[1] + B22 * W[2]);
+    } else {
+        // fp32 (the step): B applied as its three plane rotations on pairs of components (packed
+        // fp32) rather than formed; only its third column (gravity, landing gear) is needed.
+        const V2<R> b12_22 = c1 * V2<R>{s0, c0};
+        f.B02 = -s1;
+        f.B12 = b12_22.x;
+        f.B22 = b12_22.y;
+        const R sq_cr = s0 * q + c0 * r;
+        f.phid = p + t1 * sq_cr;
+        f.thd = c0 * q - s0 * r;
+        f.psid = ic1 * sq_cr;
+        // ned = B^T uvw = Rz^T Ry^T Rx^T uvw
+        const V2<R> yz1 = vv * V2<R>{c0, s0} + ww * V2<R>{-s0, c0};        // Rx^T: (y, z)
+        const V2<R> xz2 = uu * V2<R>{c1, -s1} + yz1.y * V2<R>{s1, c1};     // Ry^T: (x, z)
+        const V2<R> n01 = xz2.x * V2<R>{c2, s2} + yz1.x * V2<R>{-s2, c2};  // Rz^T: (x, y)
+        f.n0 = n01.x;
+        f.n1 = n01.y;
+        f.n2 = xz2.y;
+        // uvw_air = uvw - B W = uvw - Rx Ry Rz W
+        const V2<R> ab = W[0] * V2<R>{c2, -s2} + W[1] * V2<R>{s2, c2};     // Rz W: (x, y)
+        const V2<R> xg = ab.x * V2<R>{c1, s1} + W[2] * V2<R>{-s1, c1};     // Ry: (x, z)
+        const V2<R> yz = xg.y * V2<R>{s0, c0} + ab.y * V2<R>{c0, -s0};     // Rx: (y, z)
+        f.ua = uu - xg.x;
+        f.va = vv - yz.x;
+        f.wa = ww - yz.y;
+    }
     f.rho = P.ro_sea * m_pow((R)1 + P.lapse_t0 * s[17], P.rho_exp);
     f.irho = m_rcp(f.rho);
     // z + h with the large cancellation first (Ground::zh): the stiff gear spring K * (pos_z + h)
