@@ -8,9 +8,11 @@ import re
 import shutil
 import sys
 
-# step_kernel<TASK, ETA, NT, FEAT, MULTI, BAKED>: the per-step launch (MULTI false) is the judged
-# kernel; hg_rollout's multi-step launches (MULTI true) are summarised separately.
-SINGLE = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, (true|false)>")
+# step_kernel<TASK, ETA, NT, FEAT, MULTI, BAKED>: the per-step launch of the specialised kernel
+# (MULTI false, BAKED true) is the judged kernel; bench.py's generic-kernel secondary figure
+# (BAKED false) and hg_rollout's multi-step launches (MULTI true) are summarised separately.
+SINGLE = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, true>")
+GENERIC = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, false>")
 MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true, (true|false)>")
 
 d, tag, n, dt = sys.argv[1], sys.argv[2], int(sys.argv[3]), float(sys.argv[4])
@@ -20,7 +22,7 @@ os.makedirs(prof, exist_ok=True)
 stats = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
 if stats:
     shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
-agg, durs, mdurs = {}, [], []
+agg, durs, mdurs, gdurs = {}, [], [], []
 for f in glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         if SINGLE.search(r.get("Kernel_Name", "")):
@@ -31,10 +33,15 @@ for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursiv
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         elif MULTI.search(r["Kernel_Name"]):
             mdurs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        elif GENERIC.search(r["Kernel_Name"]):
+            gdurs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
-out = {"tag": tag, "envs": n, "dt": dt, "kernel": "step_kernel<HOVER>",
+out = {"tag": tag, "envs": n, "dt": dt, "kernel": "step_kernel<HOVER, BAKED> (specialised)",
        "kernel_avg_ns_trace": sum(durs) / len(durs) if durs else None,
        "launches_traced": len(durs), "counters_per_launch": mean}
+if gdurs:
+    out["generic_kernel_avg_ns_trace"] = sum(gdurs) / len(gdurs)
+    out["generic_launches_traced"] = len(gdurs)
 if mdurs:
     out["rollout_kernel_avg_ns_trace"] = sum(mdurs) / len(mdurs)
     out["rollout_launches_traced"] = len(mdurs)
