@@ -899,6 +899,28 @@ int hg_debug_timing(void* dst, int64_t bytes) {
 
 int32_t hg_abi_version(void) { return HG_ABI_VERSION; }
 
+int32_t hg_host_alloc(int64_t bytes, void** host, void** dev) {
+    if (!host || !dev || bytes <= 0) return fail(HG_E_INVALID, "hg_host_alloc: bad arguments");
+    *host = nullptr;
+    *dev = nullptr;
+    void* h = nullptr;
+    HIP_TRY(hipHostMalloc(&h, (size_t)bytes, hipHostMallocMapped | hipHostMallocCoherent));
+    void* d = nullptr;
+    const hipError_t err = hipHostGetDevicePointer(&d, h, 0);
+    if (err != hipSuccess || !d) {
+        (void)hipHostFree(h);
+        return fail(HG_E_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(err));
+    }
+    memset(h, 0, (size_t)bytes);
+    *host = h;
+    *dev = d;
+    return HG_OK;
+}
+
+void hg_host_free(void* host) {
+    if (host) (void)hipHostFree(host);
+}
+
 int32_t hg_debug_params(const hg_config* cfg, int32_t rows, int32_t cols, int32_t baked_only, void* out,
                         int64_t bytes) {
     if (!cfg || !out || bytes != (int64_t)sizeof(Params<float>)) return fail(HG_E_INVALID, "hg_debug_params: bad arguments");

@@ -108,6 +108,8 @@ _SIGS = {
     "hg_debug_params": (ctypes.c_int32, [ctypes.POINTER(hg_config), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                          _P, ctypes.c_int64]),
     "hg_config_is_baked": (ctypes.c_int32, [ctypes.POINTER(hg_config), ctypes.c_int32, ctypes.c_int32]),
+    "hg_host_alloc": (ctypes.c_int32, [ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_void_p)]),
+    "hg_host_free": (None, [_P]),
 }
 EXPORTED_SYMBOLS = tuple(_SIGS)
 

@@ -6,6 +6,8 @@ instance is a one-env `HeliVecEnv` without auto-reset (the reference never reset
 its step runs in the same gfx950 kernel as the batched env.  Rendering (the reference's OpenGL
 window) is not part of this package: render() raises NotImplementedError.
 """
+import ctypes
+
 import numpy as np
 
 from . import _abi, config
@@ -16,6 +18,8 @@ class Heli:
     """helicopter.py:28 — base task: reward 0, never succeeds on its own."""
 
     _task = "heli"
+    _IO = {"act": 0, "obs": 16, "rew": 96, "flags": 112}   # host-mapped I/O block layout (16 B aligned)
+    _IO_BYTES = 128
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": config.FPS}
     default_max_time = config.DEFAULT_MAX_TIME
     default_trim_cond = dict(config.DEFAULT_TRIM_COND)
@@ -29,14 +33,20 @@ class Heli:
         self.max_time = self._env.max_time
         self.success_duration = self.max_time / 4
         self.task_duration = self.max_time / 4
-        t = self._env.torch
-        self._act = t.zeros((1, 4), dtype=t.float32, device=self._env.device)
-        # pinned host staging: one async H2D copy of the action, async D2H copies of the results
-        # and a single stream synchronisation per step
-        self._h_act = t.zeros((1, 4), dtype=t.float32).pin_memory()
-        self._h_obs = t.zeros((1, 17), dtype=t.float32).pin_memory()
-        self._h_rew = t.zeros((1,), dtype=t.float32).pin_memory()
-        self._h_flags = t.zeros((3,), dtype=t.uint8).pin_memory()
+        # Host-mapped I/O (hg_host_alloc): the kernel reads the action from and writes the
+        # observation, reward and flags to pinned host memory directly, so a step is one launch
+        # and one stream synchronisation, with no copies.
+        lib = self._env.lib
+        host, dev = ctypes.c_void_p(), ctypes.c_void_p()
+        _abi.check(lib.hg_host_alloc(self._IO_BYTES, ctypes.byref(host), ctypes.byref(dev)), lib)
+        self._io_host, self._io_dev = host.value, dev.value
+        buf = (ctypes.c_uint8 * self._IO_BYTES).from_address(self._io_host)
+        raw = np.frombuffer(buf, dtype=np.uint8)
+        o = self._IO
+        self._io_act = raw[o["act"]:o["act"] + 16].view(np.float32)
+        self._io_obs = raw[o["obs"]:o["obs"] + 68].view(np.float32)
+        self._io_rew = raw[o["rew"]:o["rew"] + 4].view(np.float32)
+        self._io_flags = raw[o["flags"]:o["flags"] + 3]
 
     # setters (helicopter.py:89-111)
     def set_max_time(self, max_time=None):
@@ -71,25 +81,26 @@ class Heli:
     def step(self, actions):
         """helicopter.py:192-206 -> (obs, reward, terminated, truncated, info)."""
         e = self._env
-        self._h_act.numpy()[0] = np.asarray(actions, dtype=np.float32).reshape(4)
-        self._act.copy_(self._h_act, non_blocking=True)
-        e.step_async(self._act, with_reset_info=False)
-        self._h_obs.copy_(e.obs, non_blocking=True)
-        self._h_rew.copy_(e.reward, non_blocking=True)
-        self._h_flags[0:1].copy_(e.terminated_u8, non_blocking=True)
-        self._h_flags[1:2].copy_(e.truncated_u8, non_blocking=True)
-        self._h_flags[2:3].copy_(e.info_u8, non_blocking=True)
-        e.torch.cuda.current_stream(e.device).synchronize()
-        fl = self._h_flags.numpy()
+        self._io_act[:] = np.asarray(actions, dtype=np.float32).reshape(4)
+        d, o = self._io_dev, self._IO
+        stream = e.torch.cuda.current_stream(e.device)
+        e._check(e.lib.hg_step(e._h, d + o["act"], d + o["obs"], d + o["rew"], d + o["flags"],
+                               d + o["flags"] + 1, d + o["flags"] + 2, None, None, None, None,
+                               ctypes.c_void_p(stream.cuda_stream)))
+        stream.synchronize()
+        fl = self._io_flags
         bits = int(fl[2])
         info = {"failed": bool(bits & _abi.HG_INFO_FAILED), "successed": bool(bits & _abi.HG_INFO_SUCCESSED),
                 "time_up": bool(bits & _abi.HG_INFO_TIME_UP)}
-        return self._h_obs.numpy()[0].copy(), float(self._h_rew.numpy()[0]), bool(fl[0]), bool(fl[1]), info
+        return self._io_obs.copy(), float(self._io_rew[0]), bool(fl[0]), bool(fl[1]), info
 
     def render(self):
         raise NotImplementedError("rendering is outside heligym_amd (the reference renders with OpenGL)")
 
     def close(self):
+        if getattr(self, "_io_host", None):
+            self._env.lib.hg_host_free(self._io_host)
+            self._io_host = None
         self._env.close()
 
 

@@ -150,6 +150,14 @@ int32_t hg_debug_params(const hg_config* cfg, int32_t rows, int32_t cols, int32_
  * select the constant-specialised step kernel for it; 0 otherwise.  Host only. */
 int32_t hg_config_is_baked(const hg_config* cfg, int32_t rows, int32_t cols);
 
+/* Host memory the kernels can read and write directly (pinned, mapped, coherent): `*host` is the
+ * CPU address, `*dev` the address to pass to hg_step / hg_reset as a device pointer.  For
+ * single-env or small-batch loops that want results on the host without separate copies (the
+ * single-env drop-in: one launch and one stream synchronisation per step).  Free with
+ * hg_host_free(host). */
+int32_t hg_host_alloc(int64_t bytes, void** host, void** dev);
+void hg_host_free(void* host);
+
 /* Fill `cfg` with the AW109 / HeliHover defaults (aw109.yaml, helicopter.py:18-44,
  * helicopter_with_tasks.py:5-25).  Host only. */
 void hg_default_config(hg_config* cfg);

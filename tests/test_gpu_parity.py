@@ -802,3 +802,26 @@ def test_full_size_trajectories_vs_oracle(torch, terrain_u16):
             compared += 1
     assert compared > S * T // 4
     print(f"\n[full-size trajectories] {compared} env-steps compared, worst error / tolerance {worst:.3f}")
+
+
+def test_single_env_dropin_equals_vector_env(torch):
+    """The drop-in's host-mapped I/O path (hg_host_alloc: the kernel reads the action from and
+    writes its results to pinned host memory) gives bitwise the vector env's device-buffer results."""
+    from heligym_amd import HeliHover
+    a = HeliHover(dt=0.01, seed=4)
+    b = make_env(torch, 1, "hover", 0.01, autoreset=False, seed=4)
+    a.reset()
+    b.reset()
+    rng = np.random.RandomState(1)
+    for k in range(300):
+        act = rng.uniform(-1, 1, 4).astype(np.float32)
+        oa, ra, ta, tra, ia = a.step(act)
+        ob, rb, tb, trb, ib = b.step(torch.as_tensor(act[None], device=b.device))
+        np.testing.assert_array_equal(oa, ob[0].cpu().numpy())
+        assert ra == float(rb[0]) or (np.isnan(ra) and np.isnan(float(rb[0])))
+        assert ta == bool(tb[0]) and tra == bool(trb[0]) and ia["failed"] == bool(ib["failed"][0])
+        if ta or tra:
+            a.reset()
+            b.reset()
+    a.close()
+    b.close()
