@@ -151,8 +151,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        # HG_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several ranks on one GPU (RCCL
+        # refuses two ranks on one device); timings from such a run are not a measurement
+        backend = os.environ.get("HG_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            torch.cuda.set_device(local % torch.cuda.device_count())
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device(f"cuda:{torch.cuda.current_device()}")
