@@ -142,14 +142,26 @@ __device__ __forceinline__ const Params<float>* reload_params(const Params<float
     return (const Params<float>*)c;
 }
 
-// Per-lane access at a small byte offset from a uniform base (SGPR-base global load / store).
+// Per-lane access at a small byte offset from a uniform base (SGPR-base global load / store).  The
+// explicit global address space keeps the saddr form (`global_store_dword voff, v, s[base]`) even
+// for bases that went through an opaque copy, which would otherwise be flat stores with a 64-bit
+// VALU address add each.
+#define HG_GLOBAL __attribute__((address_space(1)))
 template <typename T>
 __device__ __forceinline__ T ld_lane(const T* __restrict__ base, uint32_t idx) {
-    return *reinterpret_cast<const T*>(reinterpret_cast<const char*>(base) + idx * (uint32_t)sizeof(T));
+    const HG_GLOBAL char* g = (const HG_GLOBAL char*)base + idx * (uint32_t)sizeof(T);
+    if constexpr (sizeof(T) == 16) {   // float4: load as a plain vector (no address-space copy ctor)
+        typedef float v4 __attribute__((ext_vector_type(4)));
+        return __builtin_bit_cast(T, *(const HG_GLOBAL v4*)g);
+    } else {
+        return *(const HG_GLOBAL T*)g;
+    }
 }
 template <bool NT, typename T>
 __device__ __forceinline__ void st_lane(T* base, uint32_t idx, T v) {
-    st_out<NT>(reinterpret_cast<T*>(reinterpret_cast<char*>(base) + idx * (uint32_t)sizeof(T)), v);
+    HG_GLOBAL T* p = (HG_GLOBAL T*)((HG_GLOBAL char*)base + idx * (uint32_t)sizeof(T));
+    if constexpr (NT && sizeof(T) >= 4) __builtin_nontemporal_store(v, p);
+    else *p = v;
 }
 
 // Observations of a step: each wave stages its 64 rows in its own LDS slice (stride 17 is
