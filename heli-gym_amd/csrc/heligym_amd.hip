@@ -175,6 +175,16 @@ __device__ __forceinline__ void store_obs_wave(float* w_obs, const float obs[17]
     const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
     const int cnt = nw > 0 ? nw * 17 : 0;
     float* out = dst + (so + w0) * 17;
+    if (nw == 64) {   // full wave: 272 float4, all LDS reads issued before the first store
+        f32x4 v[5];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) v[t] = *reinterpret_cast<const f32x4*>(w_obs + 4 * (lane + 64 * t));
+        if (lane < 16) v[4] = *reinterpret_cast<const f32x4*>(w_obs + 4 * (lane + 256));
+#pragma unroll
+        for (int t = 0; t < 4; ++t) st_out4<NT>(out + 4 * (lane + 64 * t), reinterpret_cast<const float*>(&v[t]));
+        if (lane < 16) st_out4<NT>(out + 4 * (lane + 256), reinterpret_cast<const float*>(&v[4]));
+        return;
+    }
     const int n4 = cnt >> 2;
     for (int j = lane; j < n4; j += 64) st_out4<NT>(out + 4 * j, w_obs + 4 * j);
     for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
