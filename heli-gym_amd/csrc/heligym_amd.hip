@@ -481,15 +481,19 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     ct_b = a.counters + blk0;
     asm volatile("" : "+s"(st_b), "+s"(ct_b));
     if (active) {
+        // the lane index re-materialised in this block, so that each store selects the SGPR-base
+        // form (a 32-bit lane offset) instead of a 64-bit VALU address add per store
+        uint32_t t = (uint32_t)tid;
+        asm volatile("" : "+v"(t));
 #pragma unroll
-        for (int c = 0; c < 18; ++c) st_lane<NT>(COL(st_b, c), (uint32_t)tid, hs[c]);
+        for (int c = 0; c < 18; ++c) st_lane<NT>(COL(st_b, c), t, hs[c]);
 #pragma unroll
-        for (int c = 0; c < 5; ++c) st_lane<NT>(COL(st_b, 18 + c), (uint32_t)tid, ws[c]);
+        for (int c = 0; c < 5; ++c) st_lane<NT>(COL(st_b, 18 + c), t, ws[c]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) st_lane<NT>(COL(st_b, 23 + c), (uint32_t)tid, carry[c]);
-        st_lane<NT>(COL(ct_b, 0), (uint32_t)tid, step);
-        st_lane<NT>(COL(ct_b, 1), (uint32_t)tid, succ);
-        st_lane<NT>(COL(ct_b, 2), (uint32_t)tid, epi);
+        for (int c = 0; c < 4; ++c) st_lane<NT>(COL(st_b, 23 + c), t, carry[c]);
+        st_lane<NT>(COL(ct_b, 0), t, step);
+        st_lane<NT>(COL(ct_b, 1), t, succ);
+        st_lane<NT>(COL(ct_b, 2), t, epi);
     }
 
     TSTAMP(11, "v"(tid));
