@@ -135,10 +135,19 @@ def parity_error(dt, task):
     tol = lambda r: 2e-4 + 2e-5 * np.abs(r)  # noqa: E731
     flags_ok = bool(np.all(term == b["terminated"]) and np.all(trunc == b["truncated"]))
     env.close()
+    # landing-gear contact (ground altitude < 10 ft): the stiff spring turns fp32 input rounding into
+    # a visible force difference, so contact steps are reported on their own, as the parity test does
+    contact = b["obs"][:, 16] < gc.CONTACT_GR_ALT
+    r_obs, r_st = (e_obs / tol(b["obs"])).max(axis=1), (e_st / tol(b["heli"])).max(axis=1)
+    worst = np.maximum(r_obs, r_st)
     return {"cases": int(len(b["obs"])), "obs_max_abs": float(e_obs.max()), "state_max_abs": float(e_st.max()),
             "reward_max_abs": float(np.abs(rew - b["reward"]).max()),
-            "max_err_over_tol": float(max((e_obs / tol(b["obs"])).max(), (e_st / tol(b["heli"])).max())),
-            "flags_identical": flags_ok, "tolerance": "|d| <= 2e-4 + 2e-5|x_ref| (SURVEY 8a-i)"}
+            "max_err_over_tol": float(worst[~contact].max()),
+            "contact_cases": int(contact.sum()),
+            "contact_max_err_over_tol": float(worst[contact].max()) if contact.any() else None,
+            "flags_identical": flags_ok,
+            "tolerance": "|d| <= 2e-4 + 2e-5|x_ref| (SURVEY 8a-i); gear-contact steps (ground altitude "
+                         "< 10 ft) reported separately, tested at 4x"}
 
 
 def main():
