@@ -752,6 +752,35 @@ def test_specialised_kernel_bitwise_equals_generic(torch, task, N, K):
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("N", [19_900_000])
+def test_specialised_equals_generic_past_2gb_of_state(torch, N):
+    """A batch whose state array passes 2^31 bytes (27 * N * 4), with a ragged last block: the
+    specialised kernel's SGPR-base column addressing (64-bit column bases, 32-bit lane offsets)
+    matches the generic kernel bitwise over a few steps with auto-resets."""
+    K = 3
+
+    def run(spec):
+        env = make_env(torch, N, "hover", 0.01, autoreset=True, seed=4)
+        assert env.set_specialized(spec) == spec
+        env.reset()
+        act = torch.empty((N, 4), dtype=torch.float32, device=env.device)
+        for k in range(K):
+            env.random_actions(act, seed=11, step=k)
+            act[: N // 2, 0] = -1.0
+            env.step_async(act, with_reset_info=False)
+        s, c = env.get_state()
+        res = [x.clone() for x in (env.obs, env.reward, env.terminated_u8, s, c)]
+        env.close()
+        return res
+
+    a = run(True)
+    b = run(False)
+    for x, y in zip(a, b):
+        assert torch.equal(torch.nan_to_num(x.float(), nan=7.0), torch.nan_to_num(y.float(), nan=7.0))
+    del a, b
+    torch.cuda.empty_cache()
+
+
 def test_full_size_trajectories_vs_oracle(torch, terrain_u16):
     """BASELINE config 3 size: 65 536 envs stepped 100 times from a common state with their own
     U(-1,1) actions and injected turbulence noise; 64 sampled envs replayed through the oracle from
