@@ -161,7 +161,19 @@ def f8_episodes():
     return {k.split("/", 1)[1]: d[k] for k in d.files if k.startswith("episode/")}
 
 
-VARIANTS = ("turb5", "turb7_wind", "turb0", "heavy")
+VARIANTS = ("turb5", "turb7_wind", "turb0", "heavy", "wing")
+
+
+def load_contact(dt):
+    """The landings of tests/golden/traj_contact.npz recorded at time step `dt`, shaped like a
+    traj_dt*.npz file (scenarios, dt, <name>/<key>) so single_step_batch and the trajectory tests
+    read them the same way.  Hover reward only."""
+    d = np.load(os.path.join(GOLDEN, "traj_contact.npz"), allow_pickle=False)
+    names = [str(n) for n in d["scenarios"] if abs(float(d[f"{n}/dt"]) - dt) < 1e-12]
+    v = {k: d[k] for k in d.files if k.split("/", 1)[0] in names}
+    v["scenarios"] = np.array(names)
+    v["dt"] = np.array(dt)
+    return v
 
 
 def load_variant(name):

@@ -20,6 +20,9 @@ traj_var_<v>.npz trajectories like traj_dt*.npz for modified parameter documents
                  levels 0/5/7, another mean wind, a heavier airframe with other rotor speeds), with
                  the parameter edits (JSON, flat airframe keys) so tests rebuild the same
                  configuration.
+traj_contact.npz landings run through landing-gear contact until the episode ends, with the
+                 reference's own 1-ulp sensitivity envelope per step (the calibrated contact
+                 tolerance of the trajectory tests).
 reset_f8.npz     second-episode resets (F8): the reference re-trims against the wind of the
                  last step (helicopter.py:198, helicopter_dynamics.py:66-71,491-555) -- winds,
                  reset states for several trim conditions / dt, and terminal steps of episodes
@@ -238,6 +241,12 @@ VARIANTS = {   # name -> (dt, edits of the reference yaml, scenarios (name, trim
                      ("HELI", "TR", "RPM"): 2150.0, ("HELI", "FS_CG"): 134.0},
               [("hover", {}, "trim_noise", 150), ("fwd80", {"ned_vel": [80.0, 0.0, 0.0]}, "trim_noise", 150),
                ("crash", {}, "low_collective", 300)]),
+    # A winged airframe (the AW109 has none: ZUW = 0 switches the wing off, helicopter_dynamics.py:
+    # 367): pins _calc_wn_fm (:363-383) -- stalled in hover (downwash), unstalled in forward flight.
+    "wing": (0.01, {("HELI", "WN", "ZUU"): 0.6, ("HELI", "WN", "ZUW"): -24.0, ("HELI", "WN", "ZMAX"): -14.0,
+                    ("HELI", "WN", "FS"): 150.0, ("HELI", "WN", "WL"): 60.0},
+             [("hover", {}, "trim_noise", 150), ("fwd100", {"ned_vel": [100.0, 0.0, 0.0]}, "trim_noise", 150),
+              ("random", {}, "uniform", 200)]),
 }
 
 
@@ -280,6 +289,115 @@ def gen_variant(ns, name):
         names.append(sname)
     out["scenarios"] = np.array(names)
     os.unlink(tmp.name)
+    return out
+
+
+# Trajectories that run THROUGH landing-gear contact (helicopter_dynamics.py:385-398) until the
+# episode ends: a slow descent onto the gear with the mean-wind drift (the gear's accumulated-moment
+# term, :397, then rolls the airframe over) and a faster one.  (name, dt, trim overrides, collective
+# offset from trim, steps cap, seed)
+CONTACT_SCENARIOS = [
+    ("land_slow", 0.01, {"gr_alt": 8.0}, -0.05, 1500, 401),
+    ("land_fast", 0.01, {"gr_alt": 12.0}, -0.2, 1500, 402),
+    ("land_fwd", 0.02, {"gr_alt": 8.0, "ned_vel": [15.0, 0.0, 0.0]}, -0.08, 1500, 403),
+    ("land_slow_002", 0.02, {"gr_alt": 8.0}, -0.05, 1500, 404),
+]
+CONTACT_MEMBERS = 8   # sensitivity ensemble per scenario (SURVEY 8(a) a27 method)
+
+
+def _contact_run(ns, dt, cond, dcoll, steps, seed, perturb=None, round_f32=False):
+    """One landing: trim at `cond`, then trim action with the collective offset by `dcoll` and
+    U(-0.02, 0.02) on the other three axes.  `perturb` (+-1 per heli state component) moves the
+    trimmed fp32 state by one ulp; `round_f32` rounds the heli and wind states to fp32 values after
+    every step (the storage precision of an fp32 implementation)."""
+    ns.helicopter.DT = dt
+    env = make_env(ns, dt)
+    env.set_trim_cond(cond)
+    np.random.seed(seed)
+    arng = np.random.RandomState(seed + 1000)
+    obs0, _ = env.reset()
+    init = {"state": np.asarray(env.heli_dyn.state.val, dtype=np.float64),
+            "wind_state": np.asarray(env.wind_dyn.state.val, dtype=np.float64),
+            "obs": np.asarray(obs0, dtype=np.float64), "trim_cond": trim_vec(cond),
+            "state_dots": np.asarray(env.heli_dyn.state_dots.val, dtype=np.float64),
+            "trim_action": np.asarray(env.heli_dyn.action, dtype=np.float64)}
+    if perturb is not None:
+        v = env.heli_dyn.state.val
+        assert v.dtype == np.float32
+        env.heli_dyn.state.val = np.nextafter(v, np.where(perturb > 0, np.inf, -np.inf).astype(np.float32))
+    trim_a = np.asarray(env.heli_dyn.action, dtype=np.float32)
+    rec = {k: [] for k in ["action", "eta", "wind_ned", "state", "wind_state", "obs", "state_dots", "reward_hover",
+                           "failed", "successed", "time_up", "terminated", "truncated", "success_hover"]}
+    for t in range(steps):
+        a = (trim_a + arng.uniform(-0.02, 0.02, size=4)).astype(np.float32)
+        a[0] = trim_a[0] + np.float32(dcoll)
+        obs, rew, term, trunc, info = env.step(a)
+        if round_f32:
+            for dyn in (env.heli_dyn, env.wind_dyn):
+                v = dyn.state.val
+                dyn.state.val = v.astype(np.float32).astype(v.dtype)
+        _, shv = ns.tasks.HeliHover._calculate_reward(env)
+        rec["action"].append(a.astype(np.float64))
+        rec["eta"].append(np.asarray(env.wind_dyn.eta, dtype=np.float64))
+        rec["wind_ned"].append(np.asarray(env.heli_dyn.WIND_NED, dtype=np.float64))
+        rec["state"].append(np.asarray(env.heli_dyn.state.val, dtype=np.float64))
+        rec["wind_state"].append(np.asarray(env.wind_dyn.state.val, dtype=np.float64))
+        rec["obs"].append(np.asarray(obs, dtype=np.float64))
+        rec["state_dots"].append(np.asarray(env.heli_dyn.state_dots.val, dtype=np.float64))
+        rec["reward_hover"].append(float(rew))
+        rec["success_hover"].append(bool(shv))
+        for k in ("failed", "successed", "time_up"):
+            rec[k].append(bool(info[k]))
+        rec["terminated"].append(bool(term))
+        rec["truncated"].append(bool(trunc))
+        if term or trunc:
+            break
+    return init, {k: np.array(v) for k, v in rec.items()}
+
+
+def _wrapped_diff(a, b, cols):
+    d = np.abs(a - b)
+    for c in cols:
+        d[:, c] = np.minimum(d[:, c], 2 * np.pi - d[:, c])
+    return d
+
+
+def gen_contact(ns):
+    """traj_contact.npz: each CONTACT_SCENARIOS landing recorded like run_scenario, plus the
+    reference's own sensitivity through contact: CONTACT_MEMBERS re-runs with the trimmed state
+    moved by one fp32 ulp in random directions (half of them also rounding the state to fp32 after
+    every step), same actions and noise.  sens_obs[t] / sens_state[t] = the largest deviation of
+    any member from the recorded trajectory at step t (over the steps every member reached);
+    member_end = the step at which each member's episode ended."""
+    out = {}
+    names = []
+    for name, dt, cond, dcoll, steps, seed in CONTACT_SCENARIOS:
+        init, base = _contact_run(ns, dt, cond, dcoll, steps, seed)
+        T = len(base["obs"])
+        so = np.zeros((T, 17))
+        ss = np.zeros((T, 18))
+        ends = []
+        prng = np.random.RandomState(seed + 7)
+        for m in range(CONTACT_MEMBERS):
+            sign = prng.choice([-1.0, 1.0], size=18)
+            _, mem = _contact_run(ns, dt, cond, dcoll, steps, seed, perturb=sign, round_f32=m % 2 == 1)
+            n = min(T, len(mem["obs"]))
+            ends.append(len(mem["obs"]) - 1)
+            so[:n] = np.maximum(so[:n], _wrapped_diff(mem["obs"][:n], base["obs"][:n], (7, 8, 9)))
+            ss[:n] = np.maximum(ss[:n], _wrapped_diff(mem["state"][:n], base["state"][:n], (2, 3, 4, 5, 12, 13, 14)))
+            if n < T:   # a member ended early: no envelope past its end
+                so[n:] = np.inf
+                ss[n:] = np.inf
+        first = int(np.argmax(base["obs"][:, 16] < 10.0)) if np.any(base["obs"][:, 16] < 10.0) else -1
+        print(f"contact {name}: {T} steps, first < 10 ft at {first}, member ends {ends}", flush=True)
+        out.update({f"{name}/{k}": v for k, v in base.items()})
+        out.update({f"{name}/init_{k}": v for k, v in init.items()})
+        out[f"{name}/dt"] = np.array(dt)
+        out[f"{name}/sens_obs"] = so
+        out[f"{name}/sens_state"] = ss
+        out[f"{name}/member_end"] = np.array(ends)
+        names.append(name)
+    out["scenarios"] = np.array(names)
     return out
 
 
@@ -409,8 +527,12 @@ def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     if only in (None, "f8"):
         np.savez_compressed(os.path.join(OUT, "reset_f8.npz"), **gen_f8(ns))
-    if only in (None, "variants"):
+    if only in (None, "contact"):
+        np.savez_compressed(os.path.join(OUT, "traj_contact.npz"), **gen_contact(ns))
+    if only in (None, "variants") or (only or "").startswith("variant:"):
         for v in VARIANTS:
+            if only and only.startswith("variant:") and v != only.split(":", 1)[1]:
+                continue
             np.savez_compressed(os.path.join(OUT, f"traj_var_{v}.npz"), **gen_variant(ns, v))
             print("variant", v, flush=True)
     if only is not None:
