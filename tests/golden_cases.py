@@ -27,8 +27,14 @@ def time_up_threshold(dt, max_time=40.0):
     return k
 
 
+def _npz(path):
+    """An npz read whole into a dict (NpzFile decompresses a member again on every access)."""
+    with np.load(path, allow_pickle=False) as f:
+        return {k: f[k] for k in f.files}
+
+
 def load(tag):
-    return np.load(os.path.join(GOLDEN, f"traj_dt{tag}.npz"), allow_pickle=False)
+    return _npz(os.path.join(GOLDEN, f"traj_dt{tag}.npz"))
 
 
 def single_step_batch(d, task="hover"):
@@ -168,9 +174,9 @@ def load_contact(dt):
     """The landings of tests/golden/traj_contact.npz recorded at time step `dt`, shaped like a
     traj_dt*.npz file (scenarios, dt, <name>/<key>) so single_step_batch and the trajectory tests
     read them the same way.  Hover reward only."""
-    d = np.load(os.path.join(GOLDEN, "traj_contact.npz"), allow_pickle=False)
+    d = _npz(os.path.join(GOLDEN, "traj_contact.npz"))
     names = [str(n) for n in d["scenarios"] if abs(float(d[f"{n}/dt"]) - dt) < 1e-12]
-    v = {k: d[k] for k in d.files if k.split("/", 1)[0] in names}
+    v = {k: d[k] for k in d if k.split("/", 1)[0] in names}
     v["scenarios"] = np.array(names)
     v["dt"] = np.array(dt)
     return v
@@ -182,7 +188,7 @@ def load_variant(name):
     import copy
     import json
     from heligym_amd import config
-    d = np.load(os.path.join(GOLDEN, f"traj_var_{name}.npz"), allow_pickle=False)
+    d = _npz(os.path.join(GOLDEN, f"traj_var_{name}.npz"))
     doc = copy.deepcopy(config.load_airframe("aw109"))
     doc["airframe"].update(json.loads(str(d["airframe_edits_json"])))
     return d, doc
