@@ -166,7 +166,9 @@ __device__ __forceinline__ void st_lane(T* base, uint32_t idx, T v) {
 
 // Observations of a step: each wave stages its 64 rows in its own LDS slice (stride 17 is
 // bank-conflict free) and writes them back as contiguous float4, with no block-wide barrier.
-template <bool NT>
+// MULTI (hg_rollout): step s's rows start at obs + s*N*17 floats, 16-byte aligned only when
+// N % 4 == 0 (or s % 4 == 0); unaligned rows go out as dwords.
+template <bool NT, bool MULTI>
 __device__ __forceinline__ void store_obs_wave(float* w_obs, const float obs[17], float* dst, int64_t so, int64_t w0,
                                                int64_t n, int lane) {
 #pragma unroll
@@ -175,7 +177,8 @@ __device__ __forceinline__ void store_obs_wave(float* w_obs, const float obs[17]
     const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
     const int cnt = nw > 0 ? nw * 17 : 0;
     float* out = dst + (so + w0) * 17;
-    if (nw == 64) {   // full wave: 272 float4, all LDS reads issued before the first store
+    const bool aligned = !MULTI || (((uintptr_t)out & 15) == 0);
+    if (nw == 64 && aligned) {   // full wave: 272 float4, all LDS reads issued before the first store
         f32x4 v[5];
 #pragma unroll
         for (int t = 0; t < 4; ++t) v[t] = *reinterpret_cast<const f32x4*>(w_obs + 4 * (lane + 64 * t));
@@ -185,16 +188,16 @@ __device__ __forceinline__ void store_obs_wave(float* w_obs, const float obs[17]
         if (lane < 16) st_out4<NT>(out + 4 * (lane + 256), reinterpret_cast<const float*>(&v[4]));
         return;
     }
-    const int n4 = cnt >> 2;
+    const int n4 = aligned ? cnt >> 2 : 0;
     for (int j = lane; j < n4; j += 64) st_out4<NT>(out + 4 * j, w_obs + 4 * j);
     for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
 }
 
-template <bool NT>
+template <bool NT, bool MULTI>
 __device__ __forceinline__ void store_obs(float* s_obs, const float obs[17], float* dst, int64_t so, int64_t blk0,
                                           int64_t n, int tid) {
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
-    store_obs_wave<NT>(s_obs + wv * 64 * HG_N_OBS, obs, dst, so, blk0 + wv * 64, n, tid & 63);
+    store_obs_wave<NT, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, dst, so, blk0 + wv * 64, n, tid & 63);
 }
 
 // RK4 combinations (dynamics.py:158-171) on pairs of state components, so that they issue as packed
@@ -452,14 +455,24 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
 #pragma unroll
             for (int c = 0; c < 17; ++c) obs[c] = tr[22 + c];
         }
-    } else if (do_reset) {
-        // Template<float> = heli[18] | carry[4] | obs[17], float c held by lane c
+    } else if (__ballot(do_reset)) {
+        // Template<float> = heli[18] | carry[4] | obs[17], float c held by lane c.  The readlanes run
+        // in this wave-uniform branch (every lane has loaded its template float), the selects per lane.
 #pragma unroll
-        for (int c = 0; c < 18; ++c) hs[c] = lane_value(tpl, c);
+        for (int c = 0; c < 18; ++c) {
+            const float v = lane_value(tpl, c);
+            hs[c] = do_reset ? v : hs[c];
+        }
 #pragma unroll
-        for (int c = 0; c < 4; ++c) carry[c] = lane_value(tpl, 18 + c);
+        for (int c = 0; c < 4; ++c) {
+            const float v = lane_value(tpl, 18 + c);
+            carry[c] = do_reset ? v : carry[c];
+        }
 #pragma unroll
-        for (int c = 0; c < 17; ++c) obs[c] = lane_value(tpl, 22 + c);
+        for (int c = 0; c < 17; ++c) {
+            const float v = lane_value(tpl, 22 + c);
+            obs[c] = do_reset ? v : obs[c];
+        }
     }
     if (do_reset) {
 #pragma unroll
@@ -474,7 +487,7 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
         carry[3] = obs[16];
         if (FEAT && P.autoreset_next && done) step = -1;   // reset on the next step
     }
-    store_obs<NT>(s_obs, obs, a.obs, so, blk0, n, tid);
+    store_obs<NT, MULTI>(s_obs, obs, a.obs, so, blk0, n, tid);
     }   // steps
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
     st_b = a.state + blk0;
@@ -739,7 +752,9 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
     P.time_up_steps = first_step_above(dt, c.max_time, true);
     P.success_steps = first_step_above(dt, c.max_time / 4, false);
     P.autoreset = c.autoreset ? 1 : 0;
-    P.reset_retrim = (c.autoreset && c.reset_mode == HG_RESET_RETRIM) ? 1 : 0;
+    // RETRIM: every step records its wind (the trim wind of a later reset: an auto-reset in the
+    // kernel, or hg_reset -- the single-env drop-in, whose reset() the caller issues)
+    P.reset_retrim = (c.reset_mode == HG_RESET_RETRIM) ? 1 : 0;
     P.autoreset_next = (c.autoreset && c.autoreset_mode == HG_AUTORESET_NEXT_STEP) ? 1 : 0;
     P.max_episode_steps = (c.max_episode_steps > 0 && c.max_episode_steps < INT32_MAX) ? (int32_t)c.max_episode_steps
                                                                                         : INT32_MAX;
@@ -836,6 +851,7 @@ int32_t check_config(const hg_config* c, int32_t rows, int32_t cols) {
 
 struct hg_env {
     hg_config cfg;
+    int device = 0;                          // the HIP device the handle's memory lives on
     int64_t n = 0;
     int rows = 0, cols = 0;
     std::vector<float2> hmap_host;   // {hi, lo} split of the fp64 heights
@@ -863,6 +879,20 @@ struct hg_env {
     int64_t setup_batch_cap = 0;
 };
 
+// Every entry point that touches device memory runs on the handle's device (the caller's current
+// device may be another one), and restores the caller's current device on return.
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(const hg_env* e) {
+        int cur = 0;
+        if (e && hipGetDevice(&cur) == hipSuccess && cur != e->device && hipSetDevice(e->device) == hipSuccess)
+            prev = cur;
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 // Model constants after a configuration change (create and the setters).
 static void rederive(hg_env* e) {
     e->Pd = derive<double>(e->cfg, e->rows, e->cols);
@@ -872,9 +902,12 @@ static void rederive(hg_env* e) {
 }
 
 // Upload the fp32 model constants the step kernel reads (after create and every setter).
+// Work already queued on any stream (including non-blocking ones) may still read the constants, so
+// the device is drained first; the copy itself is synchronous.
 static int32_t upload_params(hg_env* e) {
     if (!e->params_dev) return HG_OK;
-    hipError_t err = hipMemcpy(e->params_dev, &e->Pf, sizeof(e->Pf), hipMemcpyHostToDevice);
+    hipError_t err = hipDeviceSynchronize();
+    if (err == hipSuccess) err = hipMemcpy(e->params_dev, &e->Pf, sizeof(e->Pf), hipMemcpyHostToDevice);
     if (err == hipSuccess && e->pd_dev) err = hipMemcpy(e->pd_dev, &e->Pd, sizeof(e->Pd), hipMemcpyHostToDevice);
     if (err != hipSuccess) return fail(HG_E_HIP, std::string("params upload: ") + hipGetErrorString(err));
     return HG_OK;
@@ -894,8 +927,9 @@ static int32_t build_template(hg_env* e) {
     e->tmpl.carry[2] = (float)r.obs[6];
     e->tmpl.carry[3] = (float)r.obs[16];
     e->setup = trim_setup(e->Pd, e->hmap_host.data(), e->cfg.trim);
-    if (e->tmpl_dev) {   // device copies read by the step / re-trim kernels (after prior work)
-        hipError_t err = hipMemcpy(e->tmpl_dev, &e->tmpl, sizeof(e->tmpl), hipMemcpyHostToDevice);
+    if (e->tmpl_dev) {   // device copies read by the step / re-trim kernels (after all queued work)
+        hipError_t err = hipDeviceSynchronize();
+        if (err == hipSuccess) err = hipMemcpy(e->tmpl_dev, &e->tmpl, sizeof(e->tmpl), hipMemcpyHostToDevice);
         if (err == hipSuccess && e->setup_dev)
             err = hipMemcpy(e->setup_dev, &e->setup, sizeof(e->setup), hipMemcpyHostToDevice);
         if (err != hipSuccess) return fail(HG_E_HIP, std::string("template upload: ") + hipGetErrorString(err));
@@ -1051,6 +1085,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     hipError_t err;
     int dev = 0, cus = 0;
     if ((err = hipGetDevice(&dev)) != hipSuccess) return cleanup(err, "hipGetDevice");
+    e->device = dev;
     if ((err = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
         return cleanup(err, "hipDeviceGetAttribute");
     e->resident_envs = (int64_t)cus * 4 * 64;
@@ -1091,6 +1126,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
 
 void hg_destroy(hg_env* e) {
     if (!e) return;
+    DevGuard dev_guard(e);
     dfree(e->hmap);
     dfree(e->state);
     dfree(e->counters);
@@ -1110,6 +1146,7 @@ int64_t hg_num_envs(const hg_env* e) { return e ? e->n : -1; }
 
 int32_t hg_set_max_time(hg_env* e, double max_time) {
     if (!e || !(max_time > 0)) return fail(HG_E_INVALID, "bad env or max_time");
+    DevGuard dev_guard(e);
     e->cfg.max_time = max_time;
     rederive(e);
     return upload_params(e);
@@ -1124,6 +1161,7 @@ int32_t hg_set_specialized(hg_env* e, int32_t enable) {
 
 int32_t hg_set_target(hg_env* e, const hg_target* t) {
     if (!e || !t) return fail(HG_E_INVALID, "bad env or target");
+    DevGuard dev_guard(e);
     e->cfg.target = *t;
     rederive(e);
     return upload_params(e);
@@ -1131,6 +1169,7 @@ int32_t hg_set_target(hg_env* e, const hg_target* t) {
 
 int32_t hg_set_trim_cond(hg_env* e, const hg_trim_cond* tc) {
     if (!e || !tc) return fail(HG_E_INVALID, "bad env or trim cond");
+    DevGuard dev_guard(e);
     const hg_trim_cond old = e->cfg.trim;
     e->cfg.trim = *tc;
     const int32_t rc = build_template(e);
@@ -1146,6 +1185,7 @@ int32_t hg_get_template(const hg_env* e, hg_trim_result* out) {
 
 int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    DevGuard dev_guard(e);
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(reset_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->tmpl,
                        e->Pf.env_templates ? e->tmpl_env : nullptr, e->state, e->counters, mask, obs, e->n);
@@ -1175,6 +1215,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
                 uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count, int32_t* reset_index,
                 float* final_obs, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    DevGuard dev_guard(e);
     if (!actions || !obs || !reward || !terminated || !truncated)
         return fail(HG_E_INVALID, "actions/obs/reward/terminated/truncated must be device pointers");
     if (((uintptr_t)actions & 15) || ((uintptr_t)obs & 15))
@@ -1183,7 +1224,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
         return fail(HG_E_INVALID, "reset_index/final_obs need reset_count");
     hipStream_t s = (hipStream_t)stream;
     if (reset_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
-    const bool retrim = e->Pf.reset_retrim != 0;
+    const bool retrim = e->Pf.reset_retrim != 0 && e->Pf.autoreset != 0;   // auto-resets re-trimmed after the step
     if (retrim) HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
     StepArgs a;
     a.state = e->state;
@@ -1257,6 +1298,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
 int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, float* reward, uint8_t* terminated,
                    uint8_t* truncated, uint8_t* info, const float* eta, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    DevGuard dev_guard(e);
     if (nsteps < 1) return fail(HG_E_INVALID, "nsteps must be >= 1");
     if (!actions || !obs || !reward || !terminated || !truncated)
         return fail(HG_E_INVALID, "actions/obs/reward/terminated/truncated must be device pointers");
@@ -1316,6 +1358,7 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
 int32_t hg_trim_batch(hg_env* e, const float* wind, int64_t count, float* state, float* action, float* obs,
                       int32_t* status, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    DevGuard dev_guard(e);
     if (count < 0 || (count > 0 && !wind)) return fail(HG_E_INVALID, "bad wind / count");
     if (count == 0) return HG_OK;
     hgk::RetrimArgs r;
@@ -1336,6 +1379,7 @@ int32_t hg_trim_batch(hg_env* e, const float* wind, int64_t count, float* state,
 int32_t hg_trim_conds_batch(hg_env* e, const hg_trim_cond* conds, int64_t count, const float* wind, float* state,
                             float* action, float* obs, int32_t* status, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    DevGuard dev_guard(e);
     if (count < 0 || (count > 0 && !conds)) return fail(HG_E_INVALID, "bad conds / count");
     if (count == 0) return HG_OK;
     if (count > e->setup_batch_cap) {
@@ -1368,6 +1412,7 @@ int32_t hg_trim_conds_batch(hg_env* e, const hg_trim_cond* conds, int64_t count,
 
 int32_t hg_set_reset_templates(hg_env* e, const float* templates, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    DevGuard dev_guard(e);
     if (templates && e->cfg.reset_mode == HG_RESET_RETRIM)
         return fail(HG_E_INVALID, "per-env reset templates need reset_mode HG_RESET_TEMPLATE");
     if (templates) {
@@ -1383,6 +1428,7 @@ int32_t hg_set_reset_templates(hg_env* e, const float* templates, void* stream) 
 
 int32_t hg_retrim_failures(hg_env* e, int64_t* count) {
     if (!e || !count) return fail(HG_E_INVALID, "bad env or count");
+    DevGuard dev_guard(e);
     int32_t v = 0;
     HIP_TRY(hipMemcpy(&v, e->retrim_count + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
     *count = v;
@@ -1391,6 +1437,7 @@ int32_t hg_retrim_failures(hg_env* e, int64_t* count) {
 
 int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    DevGuard dev_guard(e);
     hipStream_t s = (hipStream_t)stream;
     if (state) hipLaunchKernelGGL(soa_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->state, state, kStateCols, e->n);
     if (counters)
@@ -1401,6 +1448,7 @@ int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
 
 int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    DevGuard dev_guard(e);
     hipStream_t s = (hipStream_t)stream;
     if (state) hipLaunchKernelGGL(rows_to_soa, dim3(grid_for(e->n)), dim3(kBlock), 0, s, state, e->state, kStateCols, e->n);
     if (counters)
@@ -1411,6 +1459,7 @@ int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, voi
 
 int32_t hg_random_actions(hg_env* e, float* actions, uint64_t seed, uint64_t step, float lo, float hi, void* stream) {
     if (!e || !actions) return fail(HG_E_INVALID, "env/actions is NULL");
+    DevGuard dev_guard(e);
     if ((uintptr_t)actions & 15) return fail(HG_E_INVALID, "actions must be 16-byte aligned");
     hipLaunchKernelGGL(random_actions_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream, actions,
                        e->n, e->cfg.env_offset, seed, step, lo, hi);

@@ -18,15 +18,17 @@ class Heli:
     """helicopter.py:28 — base task: reward 0, never succeeds on its own."""
 
     _task = "heli"
-    _IO = {"act": 0, "obs": 16, "rew": 96, "flags": 112}   # host-mapped I/O block layout (16 B aligned)
+    _IO = {"act": 0, "obs": 16, "rew": 96, "flags": 112, "eta": 116}   # host-mapped I/O block layout
     _IO_BYTES = 128
     metadata = {"render.modes": ["human", "rgb_array"], "video.frames_per_second": config.FPS}
     default_max_time = config.DEFAULT_MAX_TIME
     default_trim_cond = dict(config.DEFAULT_TRIM_COND)
 
     def __init__(self, heli_name: str = "aw109", dt: float = config.DT, seed: int = 0, device=None):
+        # reset_mode "retrim": like the reference, every reset() trims against the wind of the last
+        # step (helicopter.py:208-212 -> helicopter_dynamics.py:66-71; SURVEY F8), on the device
         self._env = HeliVecEnv(1, task=self._task, dt=dt, heli_name=heli_name, seed=seed, device=device,
-                               autoreset=False)
+                               autoreset=False, reset_mode="retrim")
         self.observation_space = self._env.observation_space
         self.action_space = self._env.action_space
         self.normalizers = self._env.normalizers
@@ -47,6 +49,7 @@ class Heli:
         self._io_obs = raw[o["obs"]:o["obs"] + 68].view(np.float32)
         self._io_rew = raw[o["rew"]:o["rew"] + 4].view(np.float32)
         self._io_flags = raw[o["flags"]:o["flags"] + 3]
+        self._io_eta = raw[o["eta"]:o["eta"] + 12].view(np.float32)
 
     # setters (helicopter.py:89-111)
     def set_max_time(self, max_time=None):
@@ -78,15 +81,19 @@ class Heli:
         obs, info = self._env.reset()
         return obs[0].cpu().numpy().copy(), {k: bool(v[0]) for k, v in info.items()}
 
-    def step(self, actions):
-        """helicopter.py:192-206 -> (obs, reward, terminated, truncated, info)."""
+    def step(self, actions, eta=None):
+        """helicopter.py:192-206 -> (obs, reward, terminated, truncated, info).  `eta`: optional
+        turbulence noise [3] (already scaled by 1/sqrt(dt)) instead of the in-kernel Philox draw --
+        the reference's `wind_dyn.eta` (wind_dynamics.py:49-52), for replaying recorded episodes."""
         e = self._env
         self._io_act[:] = np.asarray(actions, dtype=np.float32).reshape(4)
         d, o = self._io_dev, self._IO
+        if eta is not None:
+            self._io_eta[:] = np.asarray(eta, dtype=np.float32).reshape(3)
         stream = e.torch.cuda.current_stream(e.device)
         e._check(e.lib.hg_step(e._h, d + o["act"], d + o["obs"], d + o["rew"], d + o["flags"],
-                               d + o["flags"] + 1, d + o["flags"] + 2, None, None, None, None,
-                               ctypes.c_void_p(stream.cuda_stream)))
+                               d + o["flags"] + 1, d + o["flags"] + 2, None if eta is None else d + o["eta"],
+                               None, None, None, ctypes.c_void_p(stream.cuda_stream)))
         stream.synchronize()
         fl = self._io_flags
         bits = int(fl[2])

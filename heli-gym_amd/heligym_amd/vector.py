@@ -155,10 +155,12 @@ class HeliVecEnv:
                 "time_up": self.torch.zeros((N,), dtype=self.torch.bool, device=self.device)}
         return self.obs, info
 
-    def step_async(self, actions, eta=None, with_reset_info=True):
+    def step_async(self, actions, eta=None, with_reset_info=True, obs_out=None):
         """Launch one step on the current stream and return immediately (no host sync).
         actions: float32 [N,4] device tensor.  eta: optional float32 [N,3] injected turbulence noise
-        (already scaled by 1/sqrt(dt)), else in-kernel Philox."""
+        (already scaled by 1/sqrt(dt)), else in-kernel Philox.  obs_out: optional float32 [N,17]
+        device tensor (16-byte aligned) the observations go to instead of `self.obs` (double
+        buffering, e.g. while a previous step's observations are being gathered)."""
         a = actions
         if a.dtype != self.torch.float32 or not a.is_contiguous() or a.device != self.device:
             a = a.to(device=self.device, dtype=self.torch.float32).contiguous()
@@ -169,10 +171,16 @@ class HeliVecEnv:
             e = eta.to(device=self.device, dtype=self.torch.float32).contiguous()
             if tuple(e.shape) != (self.num_envs, 3):
                 raise ValueError("eta must be [N, 3]")
-        self._keep = (a, e)
+        o = self.obs
+        if obs_out is not None:
+            if (obs_out.dtype != self.torch.float32 or obs_out.device != self.device or not obs_out.is_contiguous()
+                    or tuple(obs_out.shape) != (self.num_envs, _abi.HG_N_OBS)):
+                raise ValueError(f"obs_out must be a contiguous float32 [{self.num_envs}, 17] tensor on {self.device}")
+            o = obs_out
+        self._keep = (a, e, o)
         rs = with_reset_info and self.autoreset and self.autoreset_mode == "same_step"
         self._check(self.lib.hg_step(
-            self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward), _ptr(self.terminated_u8),
+            self._h, _ptr(a), _ptr(o), _ptr(self.reward), _ptr(self.terminated_u8),
             _ptr(self.truncated_u8), _ptr(self.info_u8), _ptr(e),
             _ptr(self.reset_count) if rs else None, _ptr(self.reset_index) if rs else None,
             _ptr(self.final_obs) if rs else None, self._stream()))

@@ -1,0 +1,52 @@
+"""bench.py's launch and multi-rank plumbing on CPU (gloo, --dry-run: no kernel runs, value null):
+`--gpus N` without a launcher starts N ranks itself, the world size is checked, the timed windows
+are max-reduced over ranks, rank 0 prints one JSON line, and N > 1 adds BASELINE config 5 (obs
+gathered to rank 0).  The GPU measurement itself is bench.py on the MI355X box."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(*args, env=None):
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--steps", "12",
+                        "--warmup", "2", "--repeats", "2", *args], capture_output=True, text=True, env=e,
+                       timeout=300, cwd=ROOT)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+def test_gpus_2_spawns_two_ranks_and_reports_config5():
+    rc, lines, err = run("--gpus", "2")
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1   # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["world_size_seen"] == 2
+    assert d["value"] is None and "dry_run" in d
+    assert d["steps"] == 12 and d["timing"]["repeats"] == 2 and len(d["timing"]["window_s"]) == 2
+    assert d["scaling"] == "weak" and d["config"]["parallelism"] == "env-shard x2"
+    c5 = d["config5"]
+    assert "1048576" in c5["workload"] and "with_gather" in c5 and "without_gather" in c5
+    assert c5["gather_bytes_per_step_to_rank0"] == 524288 * 17 * 4
+
+
+def test_gather_obs_headline_is_config5():
+    rc, lines, err = run("--gpus", "2", "--gather-obs")
+    assert rc == 0, err[-2000:]
+    d = json.loads(lines[0])
+    assert "BASELINE config 5" in d["config"]["workload"] and d["config"]["envs_per_gpu"] == 524288
+
+
+def test_world_size_mismatch_fails():
+    rc, lines, err = run("--gpus", "2", env={"WORLD_SIZE": "3"})
+    assert rc != 0 and not lines and "WORLD_SIZE=3" in err
+
+
+def test_gather_obs_needs_ranks():
+    rc, lines, err = run("--gather-obs")
+    assert rc != 0 and not lines

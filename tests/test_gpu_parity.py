@@ -696,14 +696,16 @@ def test_make_vec_registry_defaults(torch):
 
 
 @pytest.mark.parametrize("opts", [dict(), dict(eta=True), dict(max_episode_steps=37),
-                                  dict(autoreset_mode="next_step"), dict(task="forward_flight")])
+                                  dict(autoreset_mode="next_step"), dict(task="forward_flight"),
+                                  dict(n=1001), dict(n=1003, task="forward_flight")])
 def test_rollout_equals_sequential_steps(torch, opts):
     """hg_rollout (K steps per launch, state in registers) is bitwise identical to K hg_step calls:
-    observations, rewards, flags, info bits and the final state, across auto-resets."""
+    observations, rewards, flags, info bits and the final state, across auto-resets.  Odd N: the
+    rows of steps 1..K-1 start at unaligned addresses (obs + s*N*17 floats)."""
     opts = dict(opts)
     use_eta = opts.pop("eta", False)
     task = opts.pop("task", "hover")
-    N, K = 1000, 200
+    N, K = opts.pop("n", 1000), 200
     outs = []
     for mode in ("steps", "rollout"):
         env = make_env(torch, N, task, 0.02, autoreset=True, seed=11, **opts)
@@ -970,7 +972,7 @@ def test_single_env_dropin_equals_vector_env(torch):
     writes its results to pinned host memory) gives bitwise the vector env's device-buffer results."""
     from heligym_amd import HeliHover
     a = HeliHover(dt=0.01, seed=4)
-    b = make_env(torch, 1, "hover", 0.01, autoreset=False, seed=4)
+    b = make_env(torch, 1, "hover", 0.01, autoreset=False, seed=4, reset_mode="retrim")   # as the drop-in
     a.reset()
     b.reset()
     rng = np.random.RandomState(1)
@@ -986,3 +988,63 @@ def test_single_env_dropin_equals_vector_env(torch):
             b.reset()
     a.close()
     b.close()
+
+
+def test_setters_wait_for_queued_side_stream_steps(torch):
+    """set_target / set_max_time while steps are still queued on a non-blocking side stream: the
+    queued steps use the old constants, the ones after the setter the new ones (the setters drain the
+    device before overwriting the constants) -- same results as with explicit synchronisation."""
+    N, K = 65536, 40
+    outs = []
+    for sync in (True, False):
+        env = make_env(torch, N, "hover", 0.01, autoreset=True, seed=5)
+        env.reset()
+        acts = torch.empty((K, N, 4), dtype=torch.float32, device=env.device)
+        for k in range(K):
+            env.random_actions(acts[k], seed=9, step=k)
+        torch.cuda.synchronize()
+        side = torch.cuda.Stream(device=env.device)
+        rec = []
+        with torch.cuda.stream(side):
+            for k in range(K):
+                if k == K // 2:
+                    if sync:
+                        side.synchronize()
+                    env.set_target({"north_loc": 150.0, "sea_alt": 3900.0})
+                    env.set_max_time(0.1)
+                env.step_async(acts[k], with_reset_info=False)
+                rec.append(torch.cat([env.obs, env.reward[:, None], env.truncated_u8[:, None].float()], 1).clone())
+        side.synchronize()
+        outs.append(torch.stack(rec).cpu().numpy())
+        env.close()
+    assert outs[0][K // 2:, :, 18].sum() > 0   # max_time 0.1 s: truncations after the setter
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_single_env_reset_retrims_like_reference(torch):
+    """The single-env drop-in's reset() after an episode is the reference's (F8): the recorded
+    crash step replayed through HeliHover.step() with the reference's noise, then reset() trims
+    against that step's wind (helicopter.py:208-212, helicopter_dynamics.py:66-71) and lands on the
+    reference's recorded reset state within contract (iii)."""
+    from heligym_amd import HeliHover
+    ep = gc.f8_episodes()
+    for e in range(len(ep["dt"])):
+        env = HeliHover(dt=float(ep["dt"][e]))
+        obs0, _ = env.reset()   # first reset: mean wind = the template
+        np.testing.assert_allclose(obs0, env._env.template()["obs"], rtol=1e-5, atol=1e-5)
+        pre = np.concatenate([ep["pre_state"][e], ep["pre_wind"][e], ep["pre_obs"][e][[4, 5, 6, 16]]])
+        env._env.set_state(pre[None].astype(np.float32),
+                           np.array([[int(ep["t"][e]), int(ep["succ_before"][e]), 0]], np.int32))
+        obs, r, term, trunc, info = env.step(ep["action"][e], eta=ep["eta"][e])
+        assert term and info["failed"]
+        obs, info = env.reset()
+        st, ctr = env._env.get_state()
+        s = st.cpu().numpy()[0].astype(np.float64)
+        err_s = np.abs(s[:18] - ep["reset_state"][e]) / (np.abs(ep["reset_state"][e]) + 1)
+        err_o = np.abs(obs.astype(np.float64) - ep["reset_obs"][e]) / (np.abs(ep["reset_obs"][e]) + 1)
+        print(f"\n[single-env reset after episode {e}] worst state {err_s.max():.2e} obs {err_o.max():.2e}")
+        assert np.all(err_s <= TRIM_REL) and np.all(err_o <= TRIM_REL)
+        # and it is not the template (the reference's second reset differs from its first)
+        assert np.abs(obs - obs0).max() > 1e-3
+        np.testing.assert_array_equal(s[18:23], 0.0)
+        env.close()
