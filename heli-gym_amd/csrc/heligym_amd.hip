@@ -4,8 +4,8 @@
 // (Heli.step, heligym/envs/helicopter.py:192-206): Dryden wind RK (k4-only), RK4 of the 18-state
 // helicopter model, task reward, termination flags and same-step auto-reset.  One thread = one
 // env.  Data layout in HBM (all written/read coalesced):
-//   state    [HG_STATE_COLS][N] fp32 SoA  (heli 18 | wind 5 | carry 4)
-//   counters [HG_COUNTER_COLS][N] i32 SoA (episode step, success steps, episode index)
+//   state    wave tiles [ceil(N/64)][30][64] 32-bit words (retrim.h tix): fp32 heli 18 | wind 5 |
+//            carry 4, then the i32 counters (episode step, success steps, episode index)
 //   actions  [N,4] fp32 (one float4 per lane)      obs [N,17] fp32 (LDS-staged, float4 stores)
 //   reward [N] fp32, terminated/truncated/info [N] u8
 // Model constants are read with scalar loads from a device copy; the terrain map (8 MiB float2
@@ -28,6 +28,10 @@
 
 using hg::Params;
 using hg::Template;
+using hgk::kCtrCol0;
+using hgk::kTileEnvs;
+using hgk::kTileWords;
+using hgk::tix;
 
 namespace {
 
@@ -50,6 +54,11 @@ int32_t fail(int32_t code, const std::string& msg) {
     } while (0)
 
 constexpr int kBlock = 256;
+#ifndef HG_STEP_BLOCK
+#define HG_STEP_BLOCK 64
+#endif
+constexpr int kStepBlock = HG_STEP_BLOCK;   // step kernel block: one or more waves, one state tile each
+static_assert(kTileEnvs % 64 == 0, "a state tile holds whole waves");
 constexpr int kStateCols = HG_STATE_COLS;
 constexpr int kCtrCols = HG_COUNTER_COLS;
 
@@ -78,8 +87,7 @@ __device__ __forceinline__ float u01(uint32_t x) {   // (0, 1)
 // ------------------------------------------------------------------------------ kernels
 
 struct StepArgs {
-    float* state;
-    int32_t* counters;
+    float* state;            // wave tiles (tix): state columns then counters
     const float2* hmap;
     const float* actions;
     float* obs;
@@ -193,12 +201,6 @@ __device__ __forceinline__ void store_obs_wave(float* w_obs, const float obs[17]
     for (int j = (n4 << 2) + lane; j < cnt; j += 64) st_out<NT>(out + j, w_obs[j]);
 }
 
-template <bool NT, bool MULTI>
-__device__ __forceinline__ void store_obs(float* s_obs, const float obs[17], float* dst, int64_t so, int64_t blk0,
-                                          int64_t n, int tid) {
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index in the block (uniform)
-    store_obs_wave<NT, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, dst, so, blk0 + wv * 64, n, tid & 63);
-}
 
 // RK4 combinations (dynamics.py:158-171) on pairs of state components, so that they issue as packed
 // fp32 (v_pk_fma_f32: two lanes' worth of fma per instruction at the issue cost of one): each
@@ -283,9 +285,9 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
 // instruction literals (baked.h), the runtime fields still read from the device copy.  All
 // compile-time, so the hot kernel has no data-independent branches to merge around.
 template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
-__global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
+__global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
                                                       const StepArgs a) {
-    __shared__ float s_obs[kBlock * HG_N_OBS];
+    __shared__ float s_obs[kStepBlock * HG_N_OBS];   // one 64-row slice per wave
     const Params<float>& P0 = *Pa;   // model constants: scalar loads from a device copy
     // BAKED: the default airframe's constants as instruction literals (baked.h); only the runtime
     // fields (dt, target, limits, flags) are loaded
@@ -294,20 +296,24 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
         PB = *Pa;
         hg::bake(PB);
     }
-    const int tid = threadIdx.x;
-    const int64_t blk0 = (int64_t)blockIdx.x * kBlock;
+    const int lane = threadIdx.x & 63;
+    const int wv = kStepBlock == 64 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
+    const int64_t tile = (int64_t)blockIdx.x * (kStepBlock / 64) + wv;
+    const int64_t blk0 = tile * 64;   // this wave's first env
+    const int tid = lane;
     const int64_t i = blk0 + tid;
     const int64_t n = a.n;
     const bool active = i < n;
-    // Addressing: uniform (SGPR) bases at this block's first env plus a small per-lane byte offset,
-    // so loads and stores use the SGPR-base form with no per-access 64-bit address arithmetic.
-    // Lanes past the end of a ragged last block read env blk0 and store nothing.
+    // Addressing: this wave's state tile (64 envs x 30 columns, contiguous) from one uniform (SGPR)
+    // base at its middle column, so every column is an immediate offset (+-3.8 KB, inside the 13-bit
+    // field) of the same SGPR-base access with the lane's byte offset: no address arithmetic per
+    // column.  Lanes past the end of a ragged last tile step its padding and store nothing; for the
+    // caller's [N]-row buffers they read row blk0.
     const uint32_t lo = (uint32_t)(active ? tid : 0);
-#define COL(ptr, c) ((ptr) + (int64_t)(c) * n)
-    // (the block bases are re-derived behind an opaque copy for the stores, so the compiler does
-    // not keep ~30 column addresses live across the whole step)
-    float* st_b = a.state + blk0;
-    int32_t* ct_b = a.counters + blk0;
+    const uint32_t lt = (uint32_t)tid;
+#define COL(ptr, c) ((ptr) + ((c) - 15) * kTileEnvs)
+    float* st_b = a.state + (blk0 / kTileEnvs) * kTileWords + (blk0 % kTileEnvs) + 15 * kTileEnvs;
+    int32_t* ct_b = reinterpret_cast<int32_t*>(st_b);
 
 #if HG_TIMING
     if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][15] = __builtin_amdgcn_s_memrealtime();
@@ -316,17 +322,17 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     // Loads in the order they are needed: position (-> terrain texel address), counters (-> noise
     // key), wind state and carry (-> wind step), then the heli state.
     float hs[18], ws[5], carry[4];
-    hs[15] = ld_lane(COL(st_b, 15), lo);
-    hs[16] = ld_lane(COL(st_b, 16), lo);
-    int32_t step = ld_lane(COL(ct_b, 0), lo), succ = ld_lane(COL(ct_b, 1), lo),
-            epi = ld_lane(COL(ct_b, 2), lo);
+    hs[15] = ld_lane(COL(st_b, 15), lt);
+    hs[16] = ld_lane(COL(st_b, 16), lt);
+    int32_t step = ld_lane(COL(ct_b, kCtrCol0 + 0), lt), succ = ld_lane(COL(ct_b, kCtrCol0 + 1), lt),
+            epi = ld_lane(COL(ct_b, kCtrCol0 + 2), lt);
 #pragma unroll
-    for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lo);   // the wind step needs these
+    for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lt);   // the wind step needs these
 #pragma unroll
-    for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lo);
+    for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lt);
 #pragma unroll
     for (int c = 0; c < 18; ++c)   // ... and the heli state streams in behind the noise and wind work
-        if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lo);
+        if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lt);
     const int nsteps = MULTI ? a.nsteps : 1;
     for (int sstep = 0; sstep < nsteps; ++sstep) {
     // MULTI: the constants are re-read (scalar cache) each step rather than kept live across the
@@ -334,7 +340,6 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
     const Params<float>& P = BAKED ? PB : (MULTI ? *reload_params(Pa) : P0);
     const int64_t so = MULTI ? (int64_t)sstep * n : 0;   // first row of this step's inputs / outputs
     const float4 act = ld_lane(reinterpret_cast<const float4*>(a.actions) + so + blk0, lo);
-    const int lane = tid & 63;
     // terrain texels under the committed position (F6): issued now, combined after the wind step
     const hg::GroundCell<float> cell_c = hg::ground_cell(P, hs[15], hs[16]);
     const hg::GroundTexels tex_c = hg::ground_fetch(a.hmap, cell_c);
@@ -487,12 +492,12 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
         carry[3] = obs[16];
         if (FEAT && P.autoreset_next && done) step = -1;   // reset on the next step
     }
-    store_obs<NT, MULTI>(s_obs, obs, a.obs, so, blk0, n, tid);
+    store_obs_wave<NT, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, a.obs, so, blk0, n, lane);
     }   // steps
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
-    st_b = a.state + blk0;
-    ct_b = a.counters + blk0;
-    asm volatile("" : "+s"(st_b), "+s"(ct_b));
+    st_b = a.state + (blk0 / kTileEnvs) * kTileWords + (blk0 % kTileEnvs) + 15 * kTileEnvs;
+    asm volatile("" : "+s"(st_b));
+    ct_b = reinterpret_cast<int32_t*>(st_b);
     if (active) {
         // the lane index re-materialised in this block, so that each store selects the SGPR-base
         // form (a 32-bit lane offset) instead of a 64-bit VALU address add per store
@@ -504,9 +509,9 @@ __global__ __launch_bounds__(kBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void
         for (int c = 0; c < 5; ++c) st_lane<NT>(COL(st_b, 18 + c), t, ws[c]);
 #pragma unroll
         for (int c = 0; c < 4; ++c) st_lane<NT>(COL(st_b, 23 + c), t, carry[c]);
-        st_lane<NT>(COL(ct_b, 0), t, step);
-        st_lane<NT>(COL(ct_b, 1), t, succ);
-        st_lane<NT>(COL(ct_b, 2), t, epi);
+        st_lane<NT>(COL(ct_b, kCtrCol0 + 0), t, step);
+        st_lane<NT>(COL(ct_b, kCtrCol0 + 1), t, succ);
+        st_lane<NT>(COL(ct_b, kCtrCol0 + 2), t, epi);
     }
 
     TSTAMP(11, "v"(tid));
@@ -542,59 +547,50 @@ __global__ __launch_bounds__(kBlock) void mask_list_kernel(const uint8_t* mask, 
 
 // Heli.reset for masked envs (helicopter.py:208-217)
 __global__ __launch_bounds__(kBlock) void reset_kernel(const Template<float> T, const float* tmpl_env, float* state,
-                                                       int32_t* counters, const uint8_t* mask, float* obs, int64_t n) {
+                                                       const uint8_t* mask, float* obs, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     if (mask && !mask[i]) return;
     // the shared template, or this env's own ([N][39] = heli 18 | carry 4 | obs 17)
     const float* tr = tmpl_env ? tmpl_env + i * kTplFloats : reinterpret_cast<const float*>(&T);
 #pragma unroll
-    for (int c = 0; c < 18; ++c) state[c * n + i] = tr[c];
+    for (int c = 0; c < 18; ++c) state[tix(i, c)] = tr[c];
 #pragma unroll
-    for (int c = 0; c < 5; ++c) state[(18 + c) * n + i] = 0.f;
+    for (int c = 0; c < 5; ++c) state[tix(i, 18 + c)] = 0.f;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) state[(23 + c) * n + i] = tr[18 + c];
-    counters[i] = 0;
-    counters[n + i] = 0;
-    counters[2 * n + i] += 1;
+    for (int c = 0; c < 4; ++c) state[tix(i, 23 + c)] = tr[18 + c];
+    int32_t* ctr = reinterpret_cast<int32_t*>(state);
+    ctr[tix(i, kCtrCol0 + 0)] = 0;
+    ctr[tix(i, kCtrCol0 + 1)] = 0;
+    ctr[tix(i, kCtrCol0 + 2)] += 1;
     if (obs) {
 #pragma unroll
         for (int c = 0; c < 17; ++c) obs[i * 17 + c] = tr[22 + c];
     }
 }
 
-__global__ __launch_bounds__(kBlock) void init_kernel(const Template<float> T, float* state, int32_t* counters,
-                                                      int64_t n) {
+// every slot of every tile, the padding of a ragged last tile included (its lanes step like the
+// others and store nothing)
+__global__ __launch_bounds__(kBlock) void init_kernel(const Template<float> T, float* state, int64_t slots) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    for (int c = 0; c < 18; ++c) state[c * n + i] = T.heli[c];
-    for (int c = 0; c < 5; ++c) state[(18 + c) * n + i] = 0.f;
-    for (int c = 0; c < 4; ++c) state[(23 + c) * n + i] = T.carry[c];
-    counters[i] = 0;
-    counters[n + i] = 0;
-    counters[2 * n + i] = 0;
+    if (i >= slots) return;
+    for (int c = 0; c < 18; ++c) state[tix(i, c)] = T.heli[c];
+    for (int c = 0; c < 5; ++c) state[tix(i, 18 + c)] = 0.f;
+    for (int c = 0; c < 4; ++c) state[tix(i, 23 + c)] = T.carry[c];
+    int32_t* ctr = reinterpret_cast<int32_t*>(state);
+    for (int c = 0; c < 3; ++c) ctr[tix(i, kCtrCol0 + c)] = 0;
 }
 
-// SoA <-> [N, cols] record transposes for get/set_state
-__global__ void soa_to_rows(const float* soa, float* rows, int cols, int64_t n) {
+// tiles <-> [N, cols] records for get/set_state: columns c0 .. c0+cols-1 of the tiles (32-bit words)
+__global__ void tiles_to_rows(const uint32_t* tiles, uint32_t* rows, int c0, int cols, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    for (int c = 0; c < cols; ++c) rows[i * cols + c] = soa[c * n + i];
+    for (int c = 0; c < cols; ++c) rows[i * cols + c] = tiles[tix(i, c0 + c)];
 }
-__global__ void rows_to_soa(const float* rows, float* soa, int cols, int64_t n) {
+__global__ void rows_to_tiles(const uint32_t* rows, uint32_t* tiles, int c0, int cols, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    for (int c = 0; c < cols; ++c) soa[c * n + i] = rows[i * cols + c];
-}
-__global__ void isoa_to_rows(const int32_t* soa, int32_t* rows, int cols, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    for (int c = 0; c < cols; ++c) rows[i * cols + c] = soa[c * n + i];
-}
-__global__ void irows_to_soa(const int32_t* rows, int32_t* soa, int cols, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    for (int c = 0; c < cols; ++c) soa[c * n + i] = rows[i * cols + c];
+    for (int c = 0; c < cols; ++c) tiles[tix(i, c0 + c)] = rows[i * cols + c];
 }
 
 __global__ __launch_bounds__(kBlock) void random_actions_kernel(float* act, int64_t n, int64_t env_offset,
@@ -856,8 +852,7 @@ struct hg_env {
     int rows = 0, cols = 0;
     std::vector<float2> hmap_host;   // {hi, lo} split of the fp64 heights
     float2* hmap = nullptr;
-    float* state = nullptr;
-    int32_t* counters = nullptr;
+    float* state = nullptr;                 // wave tiles (retrim.h tix): state columns + counters
     Params<float> Pf;
     Params<double> Pd;
     Template<float> tmpl;
@@ -1076,7 +1071,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     rc = build_template(e);
     if (rc != HG_OK) { delete e; return rc; }
     auto cleanup = [&](hipError_t err, const char* what) {
-        dfree(e->hmap); dfree(e->state); dfree(e->counters); dfree(e->tmpl_dev); dfree(e->params_dev);
+        dfree(e->hmap); dfree(e->state); dfree(e->tmpl_dev); dfree(e->params_dev);
         dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_count);
         dfree(e->tmpl_env); dfree(e->setup_batch);
         delete e;
@@ -1090,8 +1085,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
         return cleanup(err, "hipDeviceGetAttribute");
     e->resident_envs = (int64_t)cus * 4 * 64;
     if ((err = hipMalloc(&e->hmap, sizeof(float2) * rows * cols)) != hipSuccess) return cleanup(err, "hipMalloc terrain");
-    if ((err = hipMalloc(&e->state, sizeof(float) * kStateCols * num_envs)) != hipSuccess) return cleanup(err, "hipMalloc state");
-    if ((err = hipMalloc(&e->counters, sizeof(int32_t) * kCtrCols * num_envs)) != hipSuccess) return cleanup(err, "hipMalloc counters");
+    if ((err = hipMalloc(&e->state, sizeof(float) * hgk::tile_words(num_envs))) != hipSuccess)
+        return cleanup(err, "hipMalloc state");
     if ((err = hipMemcpy(e->hmap, e->hmap_host.data(), sizeof(float2) * rows * cols, hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy terrain");
     if ((err = hipMalloc(&e->params_dev, sizeof(Params<float>))) != hipSuccess) return cleanup(err, "hipMalloc params");
@@ -1117,7 +1112,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
                            (float)e->Pd.wm[0], (float)e->Pd.wm[1], (float)e->Pd.wm[2]);
         if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "fill_wind_kernel");
     }
-    hipLaunchKernelGGL(init_kernel, dim3(grid_for(num_envs)), dim3(kBlock), 0, 0, e->tmpl, e->state, e->counters, num_envs);
+    const int64_t slots = hgk::tile_words(num_envs) / hgk::kTileCols;
+    hipLaunchKernelGGL(init_kernel, dim3(grid_for(slots)), dim3(kBlock), 0, 0, e->tmpl, e->state, slots);
     if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "init_kernel");
     if ((err = hipDeviceSynchronize()) != hipSuccess) return cleanup(err, "init sync");
     *out = e;
@@ -1129,7 +1125,6 @@ void hg_destroy(hg_env* e) {
     DevGuard dev_guard(e);
     dfree(e->hmap);
     dfree(e->state);
-    dfree(e->counters);
     dfree(e->tmpl_dev);
     dfree(e->params_dev);
     dfree(e->setup_dev);
@@ -1188,7 +1183,7 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
     DevGuard dev_guard(e);
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(reset_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->tmpl,
-                       e->Pf.env_templates ? e->tmpl_env : nullptr, e->state, e->counters, mask, obs, e->n);
+                       e->Pf.env_templates ? e->tmpl_env : nullptr, e->state, mask, obs, e->n);
     HIP_TRY(hipGetLastError());
     if (e->cfg.reset_mode == HG_RESET_RETRIM) {   // trim each masked env against its last wind (F8)
         HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
@@ -1228,7 +1223,6 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     if (retrim) HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
     StepArgs a;
     a.state = e->state;
-    a.counters = e->counters;
     a.hmap = e->hmap;
     a.actions = actions;
     a.obs = obs;
@@ -1248,7 +1242,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     a.n = e->n;
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;
-    const dim3 grid(grid_for(e->n)), block(kBlock);
+    const dim3 grid((unsigned)((e->n + kStepBlock - 1) / kStepBlock)), block(kStepBlock);
     const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next ||
                       e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
 #define HG_LAUNCH_STEP_NT(T, NT)                                                                                 \
@@ -1309,7 +1303,6 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     StepArgs a;
     memset(&a, 0, sizeof(a));
     a.state = e->state;
-    a.counters = e->counters;
     a.hmap = e->hmap;
     a.actions = actions;
     a.obs = obs;
@@ -1324,7 +1317,7 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grid(grid_for(e->n)), block(kBlock);
+    const dim3 grid((unsigned)((e->n + kStepBlock - 1) / kStepBlock)), block(kStepBlock);
     const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
 #define HG_LAUNCH_ROLL_NT(T, NT)                                                                                 \
     do {                                                                                                         \
@@ -1439,9 +1432,12 @@ int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
     hipStream_t s = (hipStream_t)stream;
-    if (state) hipLaunchKernelGGL(soa_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->state, state, kStateCols, e->n);
+    uint32_t* t = reinterpret_cast<uint32_t*>(e->state);
+    if (state)
+        hipLaunchKernelGGL(tiles_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, t, (uint32_t*)state, 0, kStateCols, e->n);
     if (counters)
-        hipLaunchKernelGGL(isoa_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->counters, counters, kCtrCols, e->n);
+        hipLaunchKernelGGL(tiles_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, t, (uint32_t*)counters, kCtrCol0,
+                           kCtrCols, e->n);
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }
@@ -1450,9 +1446,13 @@ int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, voi
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
     hipStream_t s = (hipStream_t)stream;
-    if (state) hipLaunchKernelGGL(rows_to_soa, dim3(grid_for(e->n)), dim3(kBlock), 0, s, state, e->state, kStateCols, e->n);
+    uint32_t* t = reinterpret_cast<uint32_t*>(e->state);
+    if (state)
+        hipLaunchKernelGGL(rows_to_tiles, dim3(grid_for(e->n)), dim3(kBlock), 0, s, (const uint32_t*)state, t, 0, kStateCols,
+                           e->n);
     if (counters)
-        hipLaunchKernelGGL(irows_to_soa, dim3(grid_for(e->n)), dim3(kBlock), 0, s, counters, e->counters, kCtrCols, e->n);
+        hipLaunchKernelGGL(rows_to_tiles, dim3(grid_for(e->n)), dim3(kBlock), 0, s, (const uint32_t*)counters, t, kCtrCol0,
+                           kCtrCols, e->n);
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }

@@ -116,9 +116,9 @@ __device__ __forceinline__ bool gauss_jordan(double* M, int l) {
 __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, int64_t env, const double x[16],
                                              const double s[18], const double ob[17]) {
     if (a.list) {
-        for (int c = 0; c < 18; ++c) a.state[(int64_t)c * a.n + env] = (float)s[c];
+        for (int c = 0; c < 18; ++c) a.state[tix(env, c)] = (float)s[c];
         const int co[4] = {4, 5, 6, 16};
-        for (int c = 0; c < 4; ++c) a.state[(int64_t)(23 + c) * a.n + env] = (float)ob[co[c]];
+        for (int c = 0; c < 4; ++c) a.state[tix(env, 23 + c)] = (float)ob[co[c]];
         if (a.obs)
             for (int c = 0; c < 17; ++c) a.obs[env * 17 + c] = (float)ob[c];
     } else {
