@@ -116,6 +116,9 @@ using ParamArg = const Params<float>* __restrict__;
 #ifndef HG_MIN_WAVES
 #define HG_MIN_WAVES 1
 #endif
+#ifndef HG_EARLY_POST   // post-step terrain texels requested right after the RK update (0: after the reward)
+#define HG_EARLY_POST 1
+#endif
 #ifndef HG_MIN_WAVES_BULK   // launches with more waves than SIMDs (not NT)
 #define HG_MIN_WAVES_BULK 1
 #endif
@@ -262,6 +265,7 @@ __device__ __forceinline__ void draw_eta(const StepArgs& a, const Params<float>&
 #ifndef HG_TIMING
 #define HG_TIMING 0
 #endif
+
 #if HG_TIMING
 #define HG_TIMING_WAVES 2048
 #define HG_TIMING_SLOTS 16
@@ -373,6 +377,12 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     rk_stage<false>(hs, k, acc, st, P.dt);
     hg::dynamics<true>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
     rk_update(hs, k, acc, P.dt6);
+#if HG_EARLY_POST
+    // the terrain texels under the post-step position (the flags' ground height), requested now so
+    // that their latency hides behind the wraps and the reward
+    const hg::GroundCell<float> cell_p = hg::ground_cell(P, hs[15], hs[16]);
+    const hg::GroundTexels tex_p = hg::ground_fetch(a.hmap, cell_p);
+#endif
     TSTAMP(8, "v"(hs[8]), "v"(hs[11]), "v"(obs[16]));
     if (FEAT && P.reset_retrim && active && !(P.autoreset_next && step < 0)) {   // F8: a reset trims against this wind
         float* wb = a.retrim_wind + 3 * blk0;
@@ -393,13 +403,16 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     hs[14] = hg::pi_bound(hs[14]);
 
     TSTAMP(9, "v"(hs[0]));
-
     // reward (helicopter_with_tasks.py) and flags (helicopter.py:201-205, 219-240)
     bool success_step = false;
     float rew = 0.f;
     if (TASK == HG_TASK_HOVER) rew = hg::reward_hover(P, hs, k, &success_step);
     if (TASK == HG_TASK_FORWARD_FLIGHT) rew = hg::reward_forward(P, hs, k, &success_step);
+#if HG_EARLY_POST
+    const hg::Ground<float> h_post = hg::ground_combine<float>(tex_p, cell_p);
+#else
     const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
+#endif
     step += 1;
     const bool failed = hg::is_failed(P, hs, k, h_post);
     TSTAMP(10, "v"(rew), "v"((int)failed));

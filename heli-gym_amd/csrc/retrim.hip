@@ -113,6 +113,63 @@ __device__ __forceinline__ bool gauss_jordan(double* M, int l) {
     return true;
 }
 
+// The same elimination with the augmented matrix in registers: lane j (0..16) holds column j of
+// [J | r] (m[i] = M[i][j]).  Per pivot step lane c publishes its column through LDS (one write,
+// one broadcast read: the step's only round trip), every lane finds the same pivot row and
+// multipliers M[i][c] from it, and each lane updates its own column -- the pivot-row division and
+// the elimination run across the 17 columns at once.  Same operations in the same order as
+// hg::solve16 (and as the LDS elimination above); an update the host skips (f == 0) is computed and
+// discarded here.
+__device__ __forceinline__ bool gauss_jordan_cols(double m[16], double* colbuf, int l) {
+    const bool own = l < 17;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        if (l == c) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) colbuf[i] = m[i];
+        }
+        lds_order();
+        double f[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) f[i] = colbuf[i];
+        lds_order();   // read before the next step's column is written
+        int p = c;     // first row of maximal |M[i][c]| among rows c..15 (strict >, as the host)
+        double mp = f[c];
+#pragma unroll
+        for (int i = c + 1; i < 16; ++i)
+            if (fabs(f[i]) > fabs(mp)) { p = i; mp = f[i]; }
+        p = __builtin_amdgcn_readfirstlane(p);   // the same in every lane
+        if (__builtin_amdgcn_readfirstlane((int)(mp == 0.0 || !isfinite(mp)))) return false;
+        if (p != c) {   // uniform: rows c and p swap in every column (one scalar branch per row)
+#pragma unroll
+            for (int i = c + 1; i < 16; ++i)
+                if (p == i) {
+                    asm volatile("" ::: "memory");   // a branch, not 8 selects per row
+                    double t = m[c];
+                    m[c] = m[i];
+                    m[i] = t;
+                    t = f[c];
+                    f[c] = f[i];
+                    f[i] = t;
+                }
+        }
+        const bool upd = own && l >= c;   // columns j >= c
+        const double piv = m[c] / mp;
+        m[c] = upd ? piv : m[c];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (i == c) continue;
+            const double t = m[i] - f[i] * m[c];
+            m[i] = (upd && f[i] != 0.0) ? t : m[i];
+        }
+    }
+    return true;
+}
+
+#ifndef HG_GJ_LDS
+#define HG_GJ_LDS 0   // 1: the LDS elimination (A/B)
+#endif
+
 __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, int64_t env, const double x[16],
                                              const double s[18], const double ob[17]) {
     if (a.list) {
@@ -138,7 +195,11 @@ __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, i
 // alone the residual at x0 in the first round.  A round is one trim_fcn latency; a trim of three
 // Newton steps takes four rounds.
 __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
+#if HG_GJ_LDS
     __shared__ double M[kGJElems];   // [J | r] of the current Newton step
+#else
+    __shared__ double colbuf[16];    // the pivot column of the current elimination step
+#endif
     const int l = threadIdx.x;
     const hg::Params<double>& P = *a.P;
     const double eps = hg::kTrimEps;
@@ -215,12 +276,17 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
                     hg::trim_fcn(P, T.base, xe, W, T.hc, ye, nullptr, nullptr, nullptr);
                 }
             }
-            // ---- Newton direction: [J | r] into LDS (lane j <= 16 holds column j), then Gauss-Jordan
+            // ---- Newton direction: lane j <= 16 holds column j of [J | r], then Gauss-Jordan
+            double mcol[16];
+#pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const double ym = shfl_d(ye[k], (l + 16) & 63);
-                const double v = l < 16 ? (ye[k] - ym) / (2 * eps) : y[k] - T.yt[k];
-                if (l < 17) M[k * 17 + l] = v;
+                mcol[k] = l < 16 ? (ye[k] - ym) / (2 * eps) : y[k] - T.yt[k];
             }
+#if HG_GJ_LDS
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (l < 17) M[k * 17 + l] = mcol[k];
             __syncthreads();
             RSTAMP(3 + 4 * round, "v"(ye[0]));
             ok = gauss_jordan(M, l);
@@ -228,6 +294,13 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
 #pragma unroll
             for (int k = 0; k < 16; ++k) dir[k] = M[k * 17 + 16];
             __syncthreads();   // dir read before the next round's matrix is written
+#else
+            RSTAMP(3 + 4 * round, "v"(mcol[0]));
+            ok = gauss_jordan_cols(mcol, colbuf, l);
+            if (!ok) break;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) dir[k] = read_lane(mcol[k], 16);
+#endif
             RSTAMP(4 + 4 * round, "v"(dir[0]));
             ++round;
         }

@@ -1048,3 +1048,43 @@ def test_single_env_reset_retrims_like_reference(torch):
         assert np.abs(obs - obs0).max() > 1e-3
         np.testing.assert_array_equal(s[18:23], 0.0)
         env.close()
+
+
+@pytest.mark.parametrize("specialised", [True, False])
+@pytest.mark.parametrize("api", ["step", "rollout"])
+def test_reset_template_broadcast_partial_wave(torch, specialised, api):
+    """Regression test for the reset-template broadcast (round-2 root cause of the 'early texel'
+    divergence): each reset lane reads the template float c from lane c with readlane.  Here only
+    lanes >= 39 of every wave reset (x beyond the map edge: failed at once), lanes 0..38, which hold
+    the template, do not.  Reading lanes from inside the divergent reset branch let the register
+    allocator reuse their template register for the non-reset path; the readlanes now sit in a
+    wave-uniform branch.  Reset rows must be the template exactly, the other rows untouched by it."""
+    N = 512
+    env = make_env(torch, N, "hover", 0.01, autoreset=True, seed=7)
+    env.set_specialized(specialised)
+    env.reset()
+    st, ctr = env.get_state()
+    st = st.cpu().numpy()
+    lane = np.arange(N) % 64
+    crash = lane >= 39
+    st[crash, 15] = 4000.0   # |x| > NS_MAX / 2 (helicopter.py:232-233)
+    env.set_state(st, ctr.cpu().numpy())
+    act = torch.zeros((N, 4), dtype=torch.float32, device=env.device)
+    if api == "step":
+        obs, rew, term, trunc, info = env.step(act)
+        obs, term = obs.cpu().numpy(), term.cpu().numpy()
+    else:
+        o, r, te, tr, inf = env.rollout(act[None])
+        obs, term = o[0].cpu().numpy(), te[0].cpu().numpy()
+    s2, c2 = env.get_state()
+    s2, c2 = s2.cpu().numpy(), c2.cpu().numpy()
+    tpl = env.template()
+    np.testing.assert_array_equal(term.astype(bool), crash)
+    np.testing.assert_array_equal(obs[crash], np.tile(tpl["obs"].astype(np.float32), (crash.sum(), 1)))
+    np.testing.assert_array_equal(s2[crash, :18], np.tile(tpl["state"].astype(np.float32), (crash.sum(), 1)))
+    np.testing.assert_array_equal(s2[crash, 18:23], 0.0)
+    np.testing.assert_array_equal(c2[crash, :2], 0)
+    # the non-reset lanes stepped normally (not overwritten with template values)
+    assert np.all(c2[~crash, 0] == 1) and np.all(np.isfinite(obs[~crash]))
+    assert not np.array_equal(obs[~crash][0], tpl["obs"].astype(np.float32))
+    env.close()
