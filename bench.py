@@ -43,6 +43,7 @@ BYTES_STATE_RW = 2 * (108 + 8)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
 REFERENCE_NUMPY_PER_CORE = 1367.0   # env-steps/s/core, reference on config 1
 CONFIG5_TOTAL = 1048576             # BASELINE configs[4]
+OUT_OF_CACHE_ENVS = 4194304         # 1.39 GB moved per launch: past the 256 MB Infinity Cache
 
 
 def parse():
@@ -474,6 +475,31 @@ def main():
                     "bytes_per_env_step": ROLLOUT_BYTES_PER_ENV_STEP + BYTES_STATE_RW / Rs,
                     "note": "open-loop action sequences (planning / data generation); same results as "
                             "hg_step, state read and written once per launch"}
+
+        if world == 1 and not args.no_secondary and not args.dry_run and args.envs < OUT_OF_CACHE_ENVS:
+            # the same step past the 256 MB Infinity Cache (1.39 GB moved per launch): HBM bytes, not
+            # fabric bytes, with its own committed PMC summary
+            Nx = OUT_OF_CACHE_ENVS
+            envx = make_env(args, torch, Nx, 0, dev)
+            bankx = action_bank(args, torch, envx, Nx, dev, B)
+            Kx = min(K, 200)
+
+            def stepx(k):
+                envx.step_async(bankx[k % B], with_reset_info=False)
+            for k in range(min(args.warmup, 20)):
+                stepx(k)
+            repx, _kx = graphs_for(torch, dev, stepx, Kx, B)
+            s_x, _, _ = timer.run(repx, 3)
+            del _kx
+            ach = Nx * BYTES_PER_ENV_STEP / (s_x / Kx) / 1e9
+            secondary["out_of_cache"] = {
+                "envs": Nx, "value": Nx * Kx / s_x, "unit": "env-steps/s", "ms_per_step": s_x / Kx * 1e3,
+                "steps": Kx, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
+                "traffic": (pmc_traffic(Nx, args.dt, args.task) or (None,))[0],
+                "traffic_source": (pmc_traffic(Nx, args.dt, args.task) or (None, None))[1],
+                "note": "working set 1.39 GB per launch, past the 256 MB MALL: the traffic is HBM bytes"}
+            envx.close()
+            del bankx
 
         if world > 1 and not args.no_config5 and not args.no_secondary:
             # BASELINE config 5: 1 048 576 envs over the ranks, with and without the gather to rank 0

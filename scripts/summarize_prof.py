@@ -16,6 +16,7 @@ GENERIC = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false)
 MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true, (true|false)>")
 
 d, tag, n, dt = sys.argv[1], sys.argv[2], int(sys.argv[3]), float(sys.argv[4])
+task = sys.argv[5] if len(sys.argv) > 5 else "hover"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 prof = os.path.join(root, "profiles")
 os.makedirs(prof, exist_ok=True)
@@ -36,7 +37,7 @@ for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursiv
         elif GENERIC.search(r["Kernel_Name"]):
             gdurs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
-out = {"tag": tag, "envs": n, "dt": dt, "kernel": "step_kernel<HOVER, BAKED> (specialised)",
+out = {"tag": tag, "envs": n, "dt": dt, "task": task, "kernel": "step_kernel<HOVER, BAKED> (specialised)",
        "kernel_avg_ns_trace": sum(durs) / len(durs) if durs else None,
        "launches_traced": len(durs), "counters_per_launch": mean}
 if gdurs:
@@ -53,7 +54,11 @@ if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     out["hbm_bytes_per_launch"] = rd + wr
     out["hbm_read_bytes_per_launch"] = rd
     out["hbm_write_bytes_per_launch"] = wr
-    out["traffic_note"] = "2*FETCH_SIZE + WRITE_SIZE (KiB*1024), gfx950 FETCH_SIZE x2 correction"
+    out["traffic_note"] = ("2*FETCH_SIZE + WRITE_SIZE (KiB*1024), the gfx950 FETCH_SIZE x2 correction, checked for "
+                           "this kernel's 4-B and 16-B-per-lane accesses on known byte counts in "
+                           "profiles/*_pmc_calibration.json")
+    out["impl_bytes_per_launch"] = n * (136 + 195)
+    out["algorithmic_bytes_per_launch"] = n * 318
 with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as f:
     json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))
