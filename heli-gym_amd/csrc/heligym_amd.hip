@@ -953,9 +953,9 @@ static inline unsigned retrim_grid(int64_t jobs) {
 
 #define PARAM_ARG(e) ((const Params<float>*)(e)->params_dev)
 
-// The default airframe's constant-specialised step (baked.h).
-#define HG_LAUNCH_SPECIALISED(T, ETA_, NT_, MULTI_)                                                        \
-    hipLaunchKernelGGL((step_kernel<T, ETA_, NT_, false, MULTI_, true>), grid, block, 0, s, PARAM_ARG(e),  \
+// The default airframe's constant-specialised step (baked.h), with or without the optional features.
+#define HG_LAUNCH_SPECIALISED(T, ETA_, NT_, FEAT_, MULTI_)                                                 \
+    hipLaunchKernelGGL((step_kernel<T, ETA_, NT_, FEAT_, MULTI_, true>), grid, block, 0, s, PARAM_ARG(e),  \
                        e->tmpl_dev, a)
 
 extern "C" {
@@ -1260,12 +1260,17 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
                       e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
 #define HG_LAUNCH_STEP_NT(T, NT)                                                                                 \
     do {                                                                                                         \
-        if (feat) {                                                                                              \
+        if (e->baked) {                                                                                          \
+            if (feat) {                                                                                          \
+                if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, true, false);                                        \
+                else HG_LAUNCH_SPECIALISED(T, false, NT, true, false);                                           \
+            } else {                                                                                             \
+                if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, false, false);                                       \
+                else HG_LAUNCH_SPECIALISED(T, false, NT, false, false);                                          \
+            }                                                                                                    \
+        } else if (feat) {                                                                                       \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
-        } else if (e->baked) {                                                                                   \
-            if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, false);                                                  \
-            else HG_LAUNCH_SPECIALISED(T, false, NT, false);                                                     \
         } else {                                                                                                 \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
@@ -1334,12 +1339,17 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
 #define HG_LAUNCH_ROLL_NT(T, NT)                                                                                 \
     do {                                                                                                         \
-        if (feat) {                                                                                              \
+        if (e->baked) {                                                                                          \
+            if (feat) {                                                                                          \
+                if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, true, true);                                         \
+                else HG_LAUNCH_SPECIALISED(T, false, NT, true, true);                                            \
+            } else {                                                                                             \
+                if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, false, true);                                        \
+                else HG_LAUNCH_SPECIALISED(T, false, NT, false, true);                                           \
+            }                                                                                                    \
+        } else if (feat) {                                                                                       \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
-        } else if (e->baked) {                                                                                   \
-            if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, true);                                                   \
-            else HG_LAUNCH_SPECIALISED(T, false, NT, true);                                                      \
         } else {                                                                                                 \
             if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
             else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \

@@ -228,7 +228,9 @@ class HeliVecEnv:
 
     @property
     def specialized(self):
-        """True when steps run the constant-specialised kernel (the default AW109 airframe)."""
+        """True when steps run a constant-specialised kernel (the default AW109 airframe's constants
+        compiled in): every step and rollout, with or without the optional features (reset info,
+        re-trim, next-step auto-reset, TimeLimit, per-env templates)."""
         return self._specialized
 
     def set_trim_cond(self, trim_cond=None):

@@ -817,17 +817,19 @@ def test_per_env_trim_conditions(torch):
     env.close()
 
 
-@pytest.mark.parametrize("task,N,K", [("hover", 4096, 300), ("forward_flight", 4096, 300),
-                                      ("hover", 300_000, 300)])   # the last: more waves than SIMDs
-def test_specialised_kernel_bitwise_equals_generic(torch, task, N, K):
+@pytest.mark.parametrize("task,N,K,feat", [("hover", 4096, 300, False), ("forward_flight", 4096, 300, False),
+                                           ("hover", 300_000, 300, False),   # more waves than SIMDs
+                                           ("hover", 4096, 300, True)])      # the feature kernels
+def test_specialised_kernel_bitwise_equals_generic(torch, task, N, K, feat):
     """The default airframe's constant-specialised kernel (csrc/baked.h: the model constants as
     instruction literals) and the generic kernel (constants loaded from the device copy) give
     bitwise-identical steps and rollouts: random actions, in-kernel turbulence, auto-resets; for a
-    batch within one wave per SIMD (non-temporal store path) and one past it."""
+    batch within one wave per SIMD (non-temporal store path) and one past it; feat: the feature
+    instantiations (reset-info compaction, TimeLimit) of both."""
     R = 50
 
     def run(spec):
-        env = make_env(torch, N, task, 0.01, autoreset=True, seed=3)
+        env = make_env(torch, N, task, 0.01, autoreset=True, seed=3, max_episode_steps=97 if feat else None)
         assert env.set_specialized(spec) == spec
         env.reset()
         act = torch.empty((N, 4), dtype=torch.float32, device=env.device)
@@ -836,9 +838,11 @@ def test_specialised_kernel_bitwise_equals_generic(torch, task, N, K):
         for k in range(K):
             env.random_actions(act, seed=9, step=k)
             act[: N // 2, 0] = -1.0   # low collective on half the envs: crashes and auto-resets
-            env.step_async(act, with_reset_info=False)
+            env.step_async(act, with_reset_info=feat)
             rew_sum += torch.nan_to_num(env.reward, nan=0.0)
             flags += env.terminated_u8.int() + 2 * env.truncated_u8.int()
+            if feat:
+                flags[:1] += env.reset_count   # the compaction's count
         bank = torch.empty((R, N, 4), dtype=torch.float32, device=env.device)
         for k in range(R):
             env.random_actions(bank[k], seed=10, step=k)
