@@ -13,8 +13,16 @@ import numpy as np
 from . import _abi, config
 from .vector import HeliVecEnv
 
+try:   # the reference's lineage, class Heli(gym.Env, EzPickle) (helicopter.py:28), when gymnasium is installed
+    import gymnasium as _gym
+    from gymnasium.utils import EzPickle as _EzPickle
+    _BASES = (_gym.Env, _EzPickle)
+except ImportError:   # gymnasium is optional: the same surface, duck-typed
+    _EzPickle = None
+    _BASES = (object,)
 
-class Heli:
+
+class Heli(*_BASES):
     """helicopter.py:28 — base task: reward 0, never succeeds on its own."""
 
     _task = "heli"
@@ -25,12 +33,14 @@ class Heli:
     default_trim_cond = dict(config.DEFAULT_TRIM_COND)
 
     def __init__(self, heli_name: str = "aw109", dt: float = config.DT, seed: int = 0, device=None):
+        if _EzPickle is not None:   # helicopter.py:48
+            _EzPickle.__init__(self, heli_name, dt, seed, device)
         # reset_mode "retrim": like the reference, every reset() trims against the wind of the last
         # step (helicopter.py:208-212 -> helicopter_dynamics.py:66-71), on the device
         self._env = HeliVecEnv(1, task=self._task, dt=dt, heli_name=heli_name, seed=seed, device=device,
                                autoreset=False, reset_mode="retrim")
-        self.observation_space = self._env.observation_space
-        self.action_space = self._env.action_space
+        self.observation_space = self._env.single_observation_space   # helicopter.py:56-57
+        self.action_space = self._env.single_action_space
         self.normalizers = self._env.normalizers
         self.max_time = self._env.max_time
         self.success_duration = self.max_time / 4
@@ -76,8 +86,10 @@ class Heli:
         self.base_reward_weight = zero if base_reward_weight is None else base_reward_weight
         self.terminal_reward_weight = zero if terminal_reward_weight is None else terminal_reward_weight
 
-    def reset(self):
-        """helicopter.py:208-217 -> (obs float32[17], info)."""
+    def reset(self, seed=None, options=None):
+        """helicopter.py:208-217 -> (obs float32[17], info).  The reference takes no arguments;
+        `seed` / `options` are accepted (and ignored: the noise is keyed by the constructor's seed)
+        so that gymnasium's wrappers, which pass them, work."""
         obs, info = self._env.reset()
         return obs[0].cpu().numpy().copy(), {k: bool(v[0]) for k, v in info.items()}
 

@@ -48,7 +48,14 @@ OBS_NAMES = ("POWER", "LON_AIR_SPD", "LAT_AIR_SPD", "DWN_AIR_SPD", "N_VEL", "E_V
              "N_POS", "E_POS", "ALTITUDE", "GROUND_ALTITUDE")   # helicopter_dynamics.py:23-25
 
 
-class HeliVecEnv:
+try:   # gymnasium.vector.VectorEnv lineage when gymnasium is installed (optional)
+    from gymnasium.vector import VectorEnv as _VectorEnv
+    _VEC_BASES = (_VectorEnv,)
+except ImportError:
+    _VEC_BASES = (object,)
+
+
+class HeliVecEnv(*_VEC_BASES):
     """N independent helicopters (one `hg_env` handle) on one GPU.
 
     task: "hover" (HeliHover), "forward_flight" (HeliForwardFlight) or "heli" (Heli, reward 0).
@@ -113,8 +120,11 @@ class HeliVecEnv:
         self.reset_count = torch.zeros((1,), dtype=i32, device=dev)
         self.reset_index = torch.empty((N,), dtype=i32, device=dev)
         self.final_obs = torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)
-        self.observation_space = _make_box(-np.inf, np.inf, (_abi.HG_N_OBS,))   # helicopter.py:56
-        self.action_space = _make_box(-1.0, 1.0, (_abi.HG_N_ACT,))              # helicopter.py:57
+        # gymnasium.vector's convention: one env's spaces (helicopter.py:56-57) and the batched ones
+        self.single_observation_space = _make_box(-np.inf, np.inf, (_abi.HG_N_OBS,))
+        self.single_action_space = _make_box(-1.0, 1.0, (_abi.HG_N_ACT,))
+        self.observation_space = _make_box(-np.inf, np.inf, (N, _abi.HG_N_OBS))
+        self.action_space = _make_box(-1.0, 1.0, (N, _abi.HG_N_ACT))
         self.normalizers = {                                                     # helicopter.py:63-68
             "t": float(np.sqrt(2 * self.cfg.af.mr_R / self.cfg.af.env_GRAV)),
             "x": 2 * self.cfg.af.mr_R,
