@@ -343,6 +343,31 @@ def gather_loop(torch, dist, env, bank, B, K, rank, world, dev, backend, overlap
     return body
 
 
+def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev, backend):
+    """BASELINE config 5 on this rank's shard: the gather loop and the plain (graph) steps."""
+    K5 = min(K, 500)
+    body = gather_loop(torch, dist, env5, bank5, B, K5, rank, world, dev, backend)
+    body(min(args.warmup, K5))
+    s_g5, _, _ = timer.run(body, R)
+
+    def step5(k):
+        env5.step_async(bank5[k % B], with_reset_info=False)
+    if args.dry_run:
+        def rep5():
+            for k in range(K5):
+                step5(k)
+    else:
+        rep5, _k5 = graphs_for(torch, dev, step5, K5, B)
+    s_n5, _, _ = timer.run(rep5, R)
+    return {"workload": f"HeliHover-v0 x {CONFIG5_TOTAL} envs sharded over {world} ranks ({n5} on rank {rank})",
+            "with_gather": {"value": CONFIG5_TOTAL * K5 / s_g5, "unit": "env-steps/s",
+                            "ms_per_step": s_g5 / K5 * 1e3,
+                            "mode": "eager, dist.gather of obs to rank 0 every step, double-buffered"},
+            "without_gather": {"value": CONFIG5_TOTAL * K5 / s_n5, "unit": "env-steps/s",
+                               "ms_per_step": s_n5 / K5 * 1e3, "mode": f"hipGraphs of {B} steps"},
+            "gather_bytes_per_step_to_rank0": (world - 1) * n5 * 17 * 4, "steps": K5}
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -356,13 +381,21 @@ def main():
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     backend = None
+    # HG_BENCH_FORCE_DIST=1: a process group (RCCL) even for one rank, so that the config-5 gather
+    # loop runs on hardware with one GPU (gather to itself) -- a rehearsal of the API usage only
+    forced = os.environ.get("HG_BENCH_FORCE_DIST") == "1" and world == 1 and not args.dry_run
+    if forced:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     if args.dry_run:
         dev = torch.device("cpu")
         torch.cuda.synchronize = lambda *a, **k: None   # noqa: E731  (no device in a dry run)
         if world > 1:
             backend = "gloo"
             dist.init_process_group("gloo")
-    elif world > 1:
+    elif world > 1 or forced:
         # HG_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several ranks on one GPU (RCCL
         # refuses two ranks on one device); timings from such a run are not a measurement
         backend = os.environ.get("HG_BENCH_BACKEND", "nccl")
@@ -376,7 +409,8 @@ def main():
     else:
         torch.cuda.set_device(0)
         dev = torch.device("cuda:0")
-    seen_world = dist.get_world_size() if world > 1 else 1
+    dist_on = world > 1 or forced
+    seen_world = dist.get_world_size() if dist_on else 1
     if seen_world != world:
         sys.exit(f"bench.py: process group has {seen_world} ranks, expected {world}")
     if args.gather_obs and world < 2:
@@ -501,40 +535,32 @@ def main():
             envx.close()
             del bankx
 
-        if world > 1 and not args.no_config5 and not args.no_secondary:
-            # BASELINE config 5: 1 048 576 envs over the ranks, with and without the gather to rank 0
+        if dist_on and not args.no_config5 and not args.no_secondary:
+            # BASELINE config 5: 1 048 576 envs over the ranks, with and without the gather to rank 0.
+            # A failure here must not cost the headline line: the ranks agree that every one of them
+            # set up its shard before any of them enters a collective.
             from heligym_amd.distributed import shard_bounds
             off5, n5 = shard_bounds(CONFIG5_TOTAL, rank, world)
-            env5 = make_env(args, torch, n5, off5, dev)
-            bank5 = action_bank(args, torch, env5, n5, dev, B)
-            K5 = min(K, 500)
-            body = gather_loop(torch, dist, env5, bank5, B, K5, rank, world, dev, backend)
-            body(min(args.warmup, K5))
-            s_g5, _, _ = timer.run(body, R)
-
-            def step5(k):
-                env5.step_async(bank5[k % B], with_reset_info=False)
-            if args.dry_run:
-                def rep5():
-                    for k in range(K5):
-                        step5(k)
+            ok, err5 = 1, None
+            try:
+                env5 = make_env(args, torch, n5, off5, dev)
+                bank5 = action_bank(args, torch, env5, n5, dev, B)
+            except Exception as e:   # e.g. out of memory on one rank
+                ok, err5 = 0, repr(e)
+            flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
+                secondary["config5"] = {"error": err5 or "another rank failed to set up its shard"}
             else:
-                rep5, _k5 = graphs_for(torch, dev, step5, K5, B)
-            s_n5, _, _ = timer.run(rep5, R)
-            secondary["config5"] = {
-                "workload": f"HeliHover-v0 x {CONFIG5_TOTAL} envs sharded over {world} ranks ({n5} on rank {rank})",
-                "with_gather": {"value": CONFIG5_TOTAL * K5 / s_g5, "unit": "env-steps/s",
-                                "ms_per_step": s_g5 / K5 * 1e3,
-                                "mode": "eager, dist.gather of obs to rank 0 every step, double-buffered"},
-                "without_gather": {"value": CONFIG5_TOTAL * K5 / s_n5, "unit": "env-steps/s",
-                                   "ms_per_step": s_n5 / K5 * 1e3, "mode": f"hipGraphs of {B} steps"},
-                "gather_bytes_per_step_to_rank0": (world - 1) * n5 * 17 * 4, "steps": K5}
-            env5.close()
+                secondary["config5"] = config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world,
+                                               dev, backend)
+                env5.close()
 
     if rank != 0:
-        if world > 1:
+        if dist_on:
             dist.destroy_process_group()
         return
+
     value = total_envs * K / sec
     # average step-kernel duration: the timed window holds exactly K step-kernel launches back to
     # back on the env's stream (graph mode) -- what rocprofv3's kernel-trace average measures
@@ -592,7 +618,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.dt, args.task, args.cpu_seconds)
     print(json.dumps(out), flush=True)
     env.close()
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -205,6 +205,11 @@ __device__ __forceinline__ void store_obs_wave(float* w_obs, const float obs[17]
 }
 
 
+// x in [-pi, pi) (fp32 pi rounds up, so the strict bounds are the fp32 values in [-pi, pi)); NaN: false
+__device__ __forceinline__ bool in_pi_range(float x) {
+    return x > -3.14159274101257324f && x < 3.14159274101257324f;
+}
+
 // RK4 combinations (dynamics.py:158-171) on pairs of state components, so that they issue as packed
 // fp32 (v_pk_fma_f32: two lanes' worth of fma per instruction at the issue cost of one): each
 // component is rounded exactly as the scalar `acc += 2k; st = hs + k h` / `hs += (acc + k) dt/6`.
@@ -394,13 +399,25 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     // latency hides behind the reward / flag work and a reset costs no round trip at the end
     const float tpl = lane < kTplFloats ? reinterpret_cast<const float*>(Tp)[lane] : 0.f;
     // step_after (helicopter_dynamics.py:73-77)
-    hs[2] = hg::pi_bound(hs[2]);
-    hs[3] = hg::pi_bound(hs[3]);
-    hs[4] = hg::pi_bound(hs[4]);
-    hs[5] = hg::pi_bound(hs[5]);
-    hs[12] = hg::pi_bound(hs[12]);
-    hs[13] = hg::pi_bound(hs[13]);
-    hs[14] = hg::pi_bound(hs[14]);
+    // utils.py pi_bound, (x + pi) % 2pi - pi.  An angle already in [-pi, pi) is kept as is -- what
+    // the reference's fp64 arithmetic returns to 1e-16, where the fp32 round trip through x + pi
+    // costs up to half an ulp of pi.  The rotor azimuths wrap in nearly every wave every step; the
+    // flapping and euler angles only in a wave-uniform branch taken when one of them left the range.
+    hs[2] = in_pi_range(hs[2]) ? hs[2] : hg::pi_bound(hs[2]);
+    hs[3] = in_pi_range(hs[3]) ? hs[3] : hg::pi_bound(hs[3]);
+    {
+        const int ang[5] = {4, 5, 12, 13, 14};
+        bool all_in = true;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) all_in = all_in && in_pi_range(hs[ang[j]]);
+        if (__any(!all_in)) {
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const float x = hs[ang[j]];
+                hs[ang[j]] = in_pi_range(x) ? x : hg::pi_bound(x);
+            }
+        }
+    }
 
     TSTAMP(9, "v"(hs[0]));
     // reward (helicopter_with_tasks.py) and flags (helicopter.py:201-205, 219-240)

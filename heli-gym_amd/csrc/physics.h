@@ -641,8 +641,9 @@ HD Loads<R> tail_loads(const Params<R>& P, const R* __restrict__ s, const Contro
         Y_VT = rh * P.vt_YMAX * m_sqrt(ua * ua + va_vt * va_vt) * va_vt;
     else
         Y_VT = rh * (P.vt_YUU * aua * ua + P.vt_YUV * aua * va_vt);
-    // ---- wing; the AW109 has none (ZUW = 0), the branch is uniform
-    R X_WN = (R)0, Z_WN = (R)0;
+    // ---- wing; the AW109 has none (ZUW = 0), the branch is uniform.  Absent loads are -0: x + (-0)
+    // is x for every x, so the sums below fold away (x + (+0) is not foldable: -0 + +0 = +0).
+    R X_WN = (R)-0.0, Z_WN = (R)-0.0;
     if (P.wn_on) {
         const R wa_w = wa - vi_mr;
         const R vta2 = ua * ua + wa_w * wa_w;
@@ -650,9 +651,9 @@ HD Loads<R> tail_loads(const Params<R>& P, const R* __restrict__ s, const Contro
         Z_WN = m_fabs(wa_w) > (R)0.3 * aua ? rh * P.wn_ZMAX * m_sqrt(vta2) * wa_w : rh * qq;
         X_WN = -rh * (R)(1.0 / kPi) * m_rcp(vta2) * qq * qq;
     }
-    const R power_wn = m_fabs(X_WN * ua);
+    const R power_wn = P.wn_on ? m_fabs(X_WN * ua) : (R)-0.0;
     // ---- landing gear.  QUIRK: the moment uses the ACCUMULATED force (:397).
-    R Fl0 = 0, Fl1 = 0, Fl2 = 0, Ml0 = 0, Ml1 = 0, Ml2 = 0;
+    R Fl0 = (R)-0.0, Fl1 = (R)-0.0, Fl2 = (R)-0.0, Ml0 = (R)-0.0, Ml1 = (R)-0.0, Ml2 = (R)-0.0;
     const R zh = f.zh, B02 = f.B02, B12 = f.B12, B22 = f.B22;
     // Contact is rare.  A gear point's pos_z + h is zh + (B^T r_g)_z <= zh + |r_g|, so no point can
     // touch while zh + max|r_g| <= -WL_CG/12 (lg_reach carries a rounding margin): the wave skips
