@@ -24,8 +24,18 @@ __device__ unsigned long long g_rt_timing[64];
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();                   \
         if (l == 0 && job == 0 && (j) < 64) g_rt_timing[(j)] = t_;                    \
     } while (0)
+// sub-phases of the first two pivot steps of one solve (slots 40..51)
+#define GJSTAMP(j, ...)                                                               \
+    do {                                                                              \
+        if (stamp && c < 2) {                                                         \
+            asm volatile("" ::__VA_ARGS__);                                           \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
+            if (l == 0) g_rt_timing[40 + 6 * c + (j)] = t_;                           \
+        }                                                                             \
+    } while (0)
 #else
 #define RSTAMP(j, ...) do { } while (0)
+#define GJSTAMP(j, ...) do { } while (0)
 #endif
 
 // HelicopterDynamics.trim (helicopter_dynamics.py:491-555) for many winds at once: the reset path of
@@ -120,50 +130,77 @@ __device__ __forceinline__ bool gauss_jordan(double* M, int l) {
 // the elimination run across the 17 columns at once.  Same operations in the same order as
 // hg::solve16 (and as the LDS elimination above); an update the host skips (f == 0) is computed and
 // discarded here.
-__device__ __forceinline__ bool gauss_jordan_cols(double m[16], double* colbuf, int l) {
-    const bool own = l < 17;
+// One pivot step C of the register Gauss-Jordan below (C a template parameter: every array index
+// is a compile-time constant).
+template <int C>
+__device__ __forceinline__ bool gj_step(double (&m)[16], double* colbuf, int l, bool stamp) {
+    constexpr int c = C;
+    (void)stamp;
+    GJSTAMP(0, "v"(m[0]));
+    if (l == c) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        if (l == c) {
+        for (int i = 0; i < 16; ++i) colbuf[i] = m[i];
+    }
+    lds_order();
+    double f[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) colbuf[i] = m[i];
-        }
-        lds_order();
-        double f[16];
+    for (int i = 0; i < 16; ++i) f[i] = colbuf[i];
+    lds_order();   // read before the next step's column is written
+    GJSTAMP(1, "v"(f[15]));
+    int p = c;     // first row of maximal |M[i][c]| among rows c..15 (strict >, as the host)
+    double mx = f[c];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) f[i] = colbuf[i];
-        lds_order();   // read before the next step's column is written
-        int p = c;     // first row of maximal |M[i][c]| among rows c..15 (strict >, as the host)
-        double mp = f[c];
+    for (int i = c + 1; i < 16; ++i)
+        if (fabs(f[i]) > fabs(mx)) { p = i; mx = f[i]; }
+    p = __builtin_amdgcn_readfirstlane(p);   // the same in every lane
+    GJSTAMP(2, "s"(p));
+    if (p != c) {   // uniform: rows c and p swap in every column (one scalar branch per row; a
+                    // binary tree of branches put the arrays in scratch memory)
 #pragma unroll
         for (int i = c + 1; i < 16; ++i)
-            if (fabs(f[i]) > fabs(mp)) { p = i; mp = f[i]; }
-        p = __builtin_amdgcn_readfirstlane(p);   // the same in every lane
-        if (__builtin_amdgcn_readfirstlane((int)(mp == 0.0 || !isfinite(mp)))) return false;
-        if (p != c) {   // uniform: rows c and p swap in every column (one scalar branch per row)
-#pragma unroll
-            for (int i = c + 1; i < 16; ++i)
-                if (p == i) {
-                    asm volatile("" ::: "memory");   // a branch, not 8 selects per row
-                    double t = m[c];
-                    m[c] = m[i];
-                    m[i] = t;
-                    t = f[c];
-                    f[c] = f[i];
-                    f[i] = t;
-                }
-        }
-        const bool upd = own && l >= c;   // columns j >= c
-        const double piv = m[c] / mp;
-        m[c] = upd ? piv : m[c];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if (i == c) continue;
-            const double t = m[i] - f[i] * m[c];
-            m[i] = (upd && f[i] != 0.0) ? t : m[i];
-        }
+            if (p == i) {
+                asm volatile("" ::: "memory");   // a branch, not 8 selects per row
+                double t = m[c];
+                m[c] = m[i];
+                m[i] = t;
+                t = f[c];
+                f[c] = f[i];
+                f[i] = t;
+            }
     }
+    const double mp = f[c];                     // the pivot, after the swap
+    if (__builtin_amdgcn_readfirstlane((int)(mp == 0.0 || !isfinite(mp)))) return false;
+    GJSTAMP(3, "v"(m[c]));
+    const bool upd = l < 17 && l >= c;   // columns j >= c
+    const double piv = m[c] / mp;
+    m[c] = upd ? piv : m[c];
+    GJSTAMP(4, "v"(m[c]));
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i == c) continue;
+        const double t = m[i] - f[i] * m[c];
+        m[i] = (upd && f[i] != 0.0) ? t : m[i];
+    }
+    GJSTAMP(5, "v"(m[0]), "v"(m[15]));
     return true;
+}
+
+template <int C>
+__device__ __forceinline__ bool gj_steps(double (&m)[16], double* colbuf, int l, bool stamp) {
+    if (!gj_step<C>(m, colbuf, l, stamp)) return false;
+    if constexpr (C < 15) return gj_steps<C + 1>(m, colbuf, l, stamp);
+    return true;
+}
+
+// The same elimination with the augmented matrix in registers: lane j (0..16) holds column j of
+// [J | r] (m[i] = M[i][j]).  Per pivot step lane c publishes its column through LDS (one write,
+// one broadcast read: the step's only round trip), every lane finds the same pivot row and
+// multipliers M[i][c] from it, and each lane updates its own column -- the pivot-row division and
+// the elimination run across the 17 columns at once.  Same operations in the same order as
+// hg::solve16 (and as the LDS elimination above); an update the host skips (f == 0) is computed and
+// discarded here.
+__device__ __forceinline__ bool gauss_jordan_cols(double (&m)[16], double* colbuf, int l, bool stamp) {
+    return gj_steps<0>(m, colbuf, l, stamp);
 }
 
 #ifndef HG_GJ_LDS
@@ -296,7 +333,7 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
             __syncthreads();   // dir read before the next round's matrix is written
 #else
             RSTAMP(3 + 4 * round, "v"(mcol[0]));
-            ok = gauss_jordan_cols(mcol, colbuf, l);
+            ok = gauss_jordan_cols(mcol, colbuf, l, job == 0 && round == 0);
             if (!ok) break;
 #pragma unroll
             for (int k = 0; k < 16; ++k) dir[k] = read_lane(mcol[k], 16);
