@@ -480,8 +480,9 @@ def main():
                 s_api, _, _ = timer.run(eager_api, 1)
                 secondary["step_api_eager"] = {
                     "value": total_envs * Ke / s_api, "unit": "env-steps/s", "ms_per_step": s_api / Ke * 1e3,
-                    "steps": Ke, "note": "HeliVecEnv.step() as an RL loop calls it: eager launch, info dict, "
-                                         "one host sync per step for the reset count"}
+                    "steps": Ke, "note": "HeliVecEnv.step() as an RL loop calls it: eager launch; its info dict "
+                                         "is lazy (fields not read here; the reset info costs a host read "
+                                         "of the reset count when read)"}
             if env.specialized and not args.generic_kernel:
                 # the generic kernel (model constants loaded, any airframe); bitwise-identical results
                 env.set_specialized(False)

@@ -39,6 +39,48 @@ def _make_box(low, high, shape):
         return Box(low, high, shape)
 
 
+class LazyInfo(dict):
+    """The info dict of HeliVecEnv.step(): keys present at once, each value computed on first
+    access (then cached).  `valid()` says whether the step's buffers still hold its values; reading
+    a field after they were reused raises instead of returning another step's data."""
+
+    def __init__(self, thunks, valid):
+        super().__init__({k: None for k in thunks})
+        self._thunks = dict(thunks)
+        self._valid = valid
+
+    def _get(self, k):
+        th = self._thunks.get(k)
+        if th is not None:
+            if not self._valid():
+                raise _abi.HeliGymError(f"info[{k!r}] read after its buffers were reused (read info before "
+                                        "the step after next)")
+            dict.__setitem__(self, k, th())
+            del self._thunks[k]
+        return dict.__getitem__(self, k)
+
+    def __getitem__(self, k):
+        return self._get(k)
+
+    def get(self, k, default=None):
+        return self._get(k) if k in self else default
+
+    def __iter__(self):
+        return iter(list(dict.keys(self)))
+
+    def items(self):
+        return [(k, self._get(k)) for k in list(dict.keys(self))]
+
+    def values(self):
+        return [self._get(k) for k in list(dict.keys(self))]
+
+    def copy(self):
+        return {k: self._get(k) for k in list(dict.keys(self))}
+
+    def __repr__(self):
+        return repr(self.copy())
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -116,10 +158,14 @@ class HeliVecEnv(*_VEC_BASES):
         self.reward = torch.empty((N,), dtype=f32, device=dev)
         self.terminated_u8 = torch.empty((N,), dtype=u8, device=dev)
         self.truncated_u8 = torch.empty((N,), dtype=u8, device=dev)
-        self.info_u8 = torch.empty((N,), dtype=u8, device=dev)
-        self.reset_count = torch.zeros((1,), dtype=i32, device=dev)
-        self.reset_index = torch.empty((N,), dtype=i32, device=dev)
-        self.final_obs = torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)
+        # info bits and reset info alternate between two buffer sets from step to step, so that the
+        # lazily evaluated info of step() stays valid until the step after next (no copies, no sync)
+        self._sets = [dict(info=torch.zeros((N,), dtype=u8, device=dev),
+                           count=torch.zeros((1,), dtype=i32, device=dev),
+                           index=torch.empty((N,), dtype=i32, device=dev),
+                           final=torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)) for _ in range(2)]
+        self._gen = 0
+        self._use_set(0)
         # gymnasium.vector's convention: one env's spaces (helicopter.py:56-57) and the batched ones
         self.single_observation_space = _make_box(-np.inf, np.inf, (_abi.HG_N_OBS,))
         self.single_action_space = _make_box(-1.0, 1.0, (_abi.HG_N_ACT,))
@@ -133,6 +179,10 @@ class HeliVecEnv(*_VEC_BASES):
         }
 
     # ------------------------------------------------------------------ plumbing
+    def _use_set(self, g):
+        b = self._sets[g & 1]
+        self.info_u8, self.reset_count, self.reset_index, self.final_obs = b["info"], b["count"], b["index"], b["final"]
+
     def _stream(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -188,6 +238,8 @@ class HeliVecEnv(*_VEC_BASES):
                 raise ValueError(f"obs_out must be a contiguous float32 [{self.num_envs}, 17] tensor on {self.device}")
             o = obs_out
         self._keep = (a, e, o)
+        self._gen += 1
+        self._use_set(self._gen)
         rs = with_reset_info and self.autoreset and self.autoreset_mode == "same_step"
         self._check(self.lib.hg_step(
             self._h, _ptr(a), _ptr(o), _ptr(self.reward), _ptr(self.terminated_u8),
@@ -197,21 +249,31 @@ class HeliVecEnv(*_VEC_BASES):
 
     def step(self, actions, eta=None):
         """Heli.step (helicopter.py:192-206) for all envs: (obs, reward, terminated, truncated, info).
-        Returned tensors are the env's buffers, overwritten by the next step."""
+        Returned tensors are the env's buffers, overwritten by the next step.  `info` is evaluated
+        lazily: a field costs its device ops (and, for the same-step reset info, a read of the reset
+        count) only when it is read, which must happen before the step after next."""
         self.step_async(actions, eta)
         t = self.torch
-        bits = self.info_u8
-        info = {"failed": (bits & _abi.HG_INFO_FAILED) != 0,
-                "successed": (bits & _abi.HG_INFO_SUCCESSED) != 0,
-                "time_up": (bits & _abi.HG_INFO_TIME_UP) != 0,
-                "success_step": (bits & _abi.HG_INFO_SUCCESS_STEP) != 0}
+        gen, bits = self._gen, self.info_u8
+        th = {"failed": lambda: (bits & _abi.HG_INFO_FAILED) != 0,
+              "successed": lambda: (bits & _abi.HG_INFO_SUCCESSED) != 0,
+              "time_up": lambda: (bits & _abi.HG_INFO_TIME_UP) != 0,
+              "success_step": lambda: (bits & _abi.HG_INFO_SUCCESS_STEP) != 0}
         if self.autoreset and self.autoreset_mode == "same_step":
-            k = int(self.reset_count.item())
-            idx = self.reset_index[:k].long()
-            order = t.argsort(idx)
-            info["reset_index"] = idx[order]
-            info["final_obs"] = self.final_obs[:k][order]
-        return self.obs, self.reward, self.terminated_u8.bool(), self.truncated_u8.bool(), info
+            cnt, index, final = self.reset_count, self.reset_index, self.final_obs
+            cache = {}
+
+            def resets():   # (sorted env ids, their terminal observations); one host read
+                if "r" not in cache:
+                    k = int(cnt.item())
+                    idx = index[:k].long()
+                    order = t.argsort(idx)
+                    cache["r"] = (idx[order], final[:k][order])
+                return cache["r"]
+            th["reset_index"] = lambda: resets()[0]
+            th["final_obs"] = lambda: resets()[1]
+        info = LazyInfo(th, lambda: self._gen - gen < 2)
+        return self.obs, self.reward, self.terminated_u8.view(t.bool), self.truncated_u8.view(t.bool), info
 
     # ------------------------------------------------------------------ setters (helicopter.py:89-111)
     def set_max_time(self, max_time=None):

@@ -1092,3 +1092,35 @@ def test_reset_template_broadcast_partial_wave(torch, specialised, api):
     assert np.all(c2[~crash, 0] == 1) and np.all(np.isfinite(obs[~crash]))
     assert not np.array_equal(obs[~crash][0], tpl["obs"].astype(np.float32))
     env.close()
+
+
+def test_lazy_info_matches_eager_and_expires(torch):
+    """HeliVecEnv.step()'s info is evaluated lazily from double-buffered device buffers: a field
+    read before the step after next equals the eager computation from that step's bits and reset
+    info; read later it raises instead of returning another step's data."""
+    from heligym_amd import HeliGymError, _abi
+    N = 4096
+    env = make_env(torch, N, "hover", 0.01, autoreset=True, seed=21)
+    env.reset()
+    act = torch.zeros((N, 4), dtype=torch.float32, device=env.device)
+    act[: N // 2, 0] = -1.0   # crashes: resets with terminal observations
+    seen = 0
+    for k in range(700):
+        obs, rew, term, trunc, info = env.step(act)
+        bits = env.info_u8.clone()
+        cnt = int(env.reset_count.item())
+        ref_idx = np.sort(env.reset_index[:cnt].cpu().numpy())
+        if k % 2:   # read one step later (still valid)
+            env.step_async(act)
+        assert set(info) == {"failed", "successed", "time_up", "success_step", "reset_index", "final_obs"}
+        np.testing.assert_array_equal(info["failed"].cpu().numpy(), ((bits & _abi.HG_INFO_FAILED) != 0).cpu().numpy())
+        np.testing.assert_array_equal(info["reset_index"].cpu().numpy(), ref_idx)
+        assert info["final_obs"].shape == (cnt, 17)
+        seen += cnt
+    assert seen > 0
+    obs, rew, term, trunc, info = env.step(act)
+    env.step_async(act)
+    env.step_async(act)
+    with pytest.raises(HeliGymError):
+        info["time_up"]
+    env.close()
