@@ -322,8 +322,10 @@ def gather_loop(torch, dist, env, bank, B, K, rank, world, dev, backend, overlap
     n = env.num_envs
     bufs = [torch.empty((n, 17), dtype=torch.float32, device=dev) for _ in range(2)]
     on_gpu = backend == "nccl"
-    gl = [torch.empty((n, 17), dtype=torch.float32, device=dev if on_gpu else "cpu") for _ in range(world)] \
-        if rank == 0 else None
+    # rank 0's destination rows, double-buffered like the observations (step k+1's gather is queued
+    # while a consumer may still read step k's)
+    gls = [[torch.empty((n, 17), dtype=torch.float32, device=dev if on_gpu else "cpu") for _ in range(world)]
+           if rank == 0 else None for _ in range(2)]
 
     def body(steps=K):
         works = [None, None]
@@ -333,7 +335,7 @@ def gather_loop(torch, dist, env, bank, B, K, rank, world, dev, backend, overlap
                 works[b].wait()
             env.step_async(bank[k % B], with_reset_info=False, obs_out=bufs[b])
             x = bufs[b] if on_gpu else bufs[b].cpu()   # gloo rehearsal: host staging
-            works[b] = dist.gather(x, gather_list=gl, dst=0, async_op=True)
+            works[b] = dist.gather(x, gather_list=gls[b], dst=0, async_op=True)
             if not overlap or not on_gpu:
                 works[b].wait()
                 works[b] = None
