@@ -21,6 +21,12 @@ def shard_bounds(total, rank, world):
     return offset, count
 
 
+def _staged(t, group):
+    """gloo collectives take host tensors: GPU rows go through the host there (the rehearsal of the
+    RCCL path on one GPU; RCCL itself moves device memory over xGMI)."""
+    return t.cpu() if t.is_cuda and dist.get_backend(group) == "gloo" else t
+
+
 def _pad_to(t, rows):
     if t.shape[0] == rows:
         return t
@@ -34,10 +40,11 @@ def all_gather_rows(local, total, group=None):
     world = dist.get_world_size(group)
     counts = [shard_bounds(total, r, world)[1] for r in range(world)]
     m = max(counts)
-    buf = torch.empty((world * m,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(buf, _pad_to(local.contiguous(), m), group=group)
+    x = _staged(_pad_to(local.contiguous(), m), group)
+    buf = torch.empty((world * m,) + tuple(local.shape[1:]), dtype=local.dtype, device=x.device)
+    dist.all_gather_into_tensor(buf, x, group=group)
     parts = [buf[r * m: r * m + counts[r]] for r in range(world)]
-    return torch.cat(parts, 0)
+    return torch.cat(parts, 0).to(local.device)
 
 
 def gather_rows(local, total, dst=0, group=None):
@@ -46,11 +53,11 @@ def gather_rows(local, total, dst=0, group=None):
     rank = dist.get_rank(group)
     counts = [shard_bounds(total, r, world)[1] for r in range(world)]
     m = max(counts)
-    x = _pad_to(local.contiguous(), m)
+    x = _staged(_pad_to(local.contiguous(), m), group)
     if rank == dst:
         bufs = [torch.empty_like(x) for _ in range(world)]
         dist.gather(x, gather_list=bufs, dst=dst, group=group)
-        return torch.cat([bufs[r][:counts[r]] for r in range(world)], 0)
+        return torch.cat([bufs[r][:counts[r]] for r in range(world)], 0).to(local.device)
     dist.gather(x, dst=dst, group=group)
     return None
 
