@@ -628,6 +628,13 @@ void or_dynamics(const or_model* m, const double s[18], const double act[4], con
 
 /* HelicopterDynamics.step: dynamics.py:158-171 + step_after (helicopter_dynamics.py:73-77).
  * s is updated in place; k4 -> dots; obs from the stage-4 input state. */
+/* Diagnostic (tests only, not the reference's semantics): round every RK stage input and the
+ * updated state to float32, as an fp32 implementation stores them -- the rounding the parity tests'
+ * altitude-ulp term is meant to bound. */
+static int g_stage_f32 = 0;
+void or_set_stage_f32(int on) { g_stage_f32 = on; }
+static inline double SR(double x) { return g_stage_f32 ? F32(x) : x; }
+
 void or_heli_step(const or_model* m, double s[18], const double act[4], const double W[3],
                   double dots[18], double obs[17], int state_f32) {
     controls u = controls_f32(&m->cfg.af, act);
@@ -635,14 +642,14 @@ void or_heli_step(const or_model* m, double s[18], const double act[4], const do
     double h_c = or_ground_height_p(m, s[15], s[16], state_f32);   /* committed xy (F6) */
     double k1[18], k2[18], k3[18], k4[18], st[18];
     or_dynamics_c(m, s, &u, W, h_c, k1, NULL);
-    for (int i = 0; i < 18; i++) st[i] = s[i] + k1[i] * (0.5 * dt);
+    for (int i = 0; i < 18; i++) st[i] = SR(s[i] + k1[i] * (0.5 * dt));
     or_dynamics_c(m, st, &u, W, h_c, k2, NULL);
-    for (int i = 0; i < 18; i++) st[i] = s[i] + k2[i] * (0.5 * dt);
+    for (int i = 0; i < 18; i++) st[i] = SR(s[i] + k2[i] * (0.5 * dt));
     or_dynamics_c(m, st, &u, W, h_c, k3, NULL);
-    for (int i = 0; i < 18; i++) st[i] = s[i] + k3[i] * dt;
+    for (int i = 0; i < 18; i++) st[i] = SR(s[i] + k3[i] * dt);
     or_dynamics_c(m, st, &u, W, h_c, k4, obs);
     for (int i = 0; i < 18; i++) {
-        s[i] = s[i] + (k1[i] + k2[i] * 2 + k3[i] * 2 + k4[i]) * (0.16666666666666666 * dt);
+        s[i] = SR(s[i] + (k1[i] + k2[i] * 2 + k3[i] * 2 + k4[i]) * (0.16666666666666666 * dt));
         dots[i] = k4[i];
     }
     s[2] = or_pi_bound(s[2]);

@@ -77,6 +77,7 @@ class Oracle:
         lib.or_rollout.restype = ctypes.c_int64
         lib.or_rollout.argtypes = [ctypes.c_void_p, ctypes.POINTER(_abi.hg_trim_result), ctypes.c_int64,
                                    ctypes.c_int64, ctypes.c_uint64, PD]
+        lib.or_set_stage_f32.argtypes = [ctypes.c_int]
         self.cfg = cfg
         self._hmap = np.ascontiguousarray(hmap_u16, dtype=np.uint16)
         self.m = lib.or_create(ctypes.byref(cfg), self._hmap.ctypes.data, self._hmap.shape[0],
@@ -152,6 +153,11 @@ class Oracle:
         self.lib.or_step(self.m, ctypes.byref(e), _dp(a), _dp(n), ctypes.byref(o))
         self.last_lg_margin = self.lib.or_diag_lg_margin()
         return o
+
+    def set_stage_f32(self, on):
+        """Diagnostic: RK stage inputs and the updated state rounded to float32 (an fp32
+        implementation's storage), for bounding that rounding's effect in the tests."""
+        self.lib.or_set_stage_f32(int(bool(on)))
 
     def rollout(self, tr, n_envs, n_steps, seed=0):
         cs = ctypes.c_double()
