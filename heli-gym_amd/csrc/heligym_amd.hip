@@ -908,10 +908,12 @@ struct hg_env {
 // device may be another one), and restores the caller's current device on return.
 struct DevGuard {
     int prev = -1;
+    bool ok = true;   // false: the handle's device could not be made current
     explicit DevGuard(const hg_env* e) {
         int cur = 0;
-        if (e && hipGetDevice(&cur) == hipSuccess && cur != e->device && hipSetDevice(e->device) == hipSuccess)
-            prev = cur;
+        if (!e || hipGetDevice(&cur) != hipSuccess || cur == e->device) return;
+        if (hipSetDevice(e->device) == hipSuccess) prev = cur;
+        else ok = false;
     }
     ~DevGuard() {
         if (prev >= 0) (void)hipSetDevice(prev);
@@ -1172,6 +1174,7 @@ int64_t hg_num_envs(const hg_env* e) { return e ? e->n : -1; }
 int32_t hg_set_max_time(hg_env* e, double max_time) {
     if (!e || !(max_time > 0)) return fail(HG_E_INVALID, "bad env or max_time");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     e->cfg.max_time = max_time;
     rederive(e);
     return upload_params(e);
@@ -1187,6 +1190,7 @@ int32_t hg_set_specialized(hg_env* e, int32_t enable) {
 int32_t hg_set_target(hg_env* e, const hg_target* t) {
     if (!e || !t) return fail(HG_E_INVALID, "bad env or target");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     e->cfg.target = *t;
     rederive(e);
     return upload_params(e);
@@ -1195,6 +1199,7 @@ int32_t hg_set_target(hg_env* e, const hg_target* t) {
 int32_t hg_set_trim_cond(hg_env* e, const hg_trim_cond* tc) {
     if (!e || !tc) return fail(HG_E_INVALID, "bad env or trim cond");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     const hg_trim_cond old = e->cfg.trim;
     e->cfg.trim = *tc;
     const int32_t rc = build_template(e);
@@ -1211,6 +1216,7 @@ int32_t hg_get_template(const hg_env* e, hg_trim_result* out) {
 int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(reset_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->tmpl,
                        e->Pf.env_templates ? e->tmpl_env : nullptr, e->state, mask, obs, e->n);
@@ -1241,6 +1247,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
                 float* final_obs, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (!actions || !obs || !reward || !terminated || !truncated)
         return fail(HG_E_INVALID, "actions/obs/reward/terminated/truncated must be device pointers");
     if (((uintptr_t)actions & 15) || ((uintptr_t)obs & 15))
@@ -1328,6 +1335,7 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
                    uint8_t* truncated, uint8_t* info, const float* eta, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (nsteps < 1) return fail(HG_E_INVALID, "nsteps must be >= 1");
     if (!actions || !obs || !reward || !terminated || !truncated)
         return fail(HG_E_INVALID, "actions/obs/reward/terminated/truncated must be device pointers");
@@ -1392,6 +1400,7 @@ int32_t hg_trim_batch(hg_env* e, const float* wind, int64_t count, float* state,
                       int32_t* status, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (count < 0 || (count > 0 && !wind)) return fail(HG_E_INVALID, "bad wind / count");
     if (count == 0) return HG_OK;
     hgk::RetrimArgs r;
@@ -1413,6 +1422,7 @@ int32_t hg_trim_conds_batch(hg_env* e, const hg_trim_cond* conds, int64_t count,
                             float* action, float* obs, int32_t* status, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (count < 0 || (count > 0 && !conds)) return fail(HG_E_INVALID, "bad conds / count");
     if (count == 0) return HG_OK;
     if (count > e->setup_batch_cap) {
@@ -1446,6 +1456,7 @@ int32_t hg_trim_conds_batch(hg_env* e, const hg_trim_cond* conds, int64_t count,
 int32_t hg_set_reset_templates(hg_env* e, const float* templates, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (templates && e->cfg.reset_mode == HG_RESET_RETRIM)
         return fail(HG_E_INVALID, "per-env reset templates need reset_mode HG_RESET_TEMPLATE");
     if (templates) {
@@ -1462,6 +1473,7 @@ int32_t hg_set_reset_templates(hg_env* e, const float* templates, void* stream) 
 int32_t hg_retrim_failures(hg_env* e, int64_t* count) {
     if (!e || !count) return fail(HG_E_INVALID, "bad env or count");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     int32_t v = 0;
     HIP_TRY(hipMemcpy(&v, e->retrim_count + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
     *count = v;
@@ -1471,6 +1483,7 @@ int32_t hg_retrim_failures(hg_env* e, int64_t* count) {
 int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     hipStream_t s = (hipStream_t)stream;
     uint32_t* t = reinterpret_cast<uint32_t*>(e->state);
     if (state)
@@ -1485,6 +1498,7 @@ int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
 int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     hipStream_t s = (hipStream_t)stream;
     uint32_t* t = reinterpret_cast<uint32_t*>(e->state);
     if (state)
@@ -1500,6 +1514,7 @@ int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, voi
 int32_t hg_random_actions(hg_env* e, float* actions, uint64_t seed, uint64_t step, float lo, float hi, void* stream) {
     if (!e || !actions) return fail(HG_E_INVALID, "env/actions is NULL");
     DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if ((uintptr_t)actions & 15) return fail(HG_E_INVALID, "actions must be 16-byte aligned");
     hipLaunchKernelGGL(random_actions_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream, actions,
                        e->n, e->cfg.env_offset, seed, step, lo, hi);

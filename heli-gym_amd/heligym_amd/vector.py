@@ -80,6 +80,11 @@ class LazyInfo(dict):
     def __repr__(self):
         return repr(self.copy())
 
+    def __eq__(self, other):
+        return self.copy() == (other.copy() if isinstance(other, LazyInfo) else other)
+
+    __hash__ = None
+
 
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
