@@ -124,14 +124,13 @@ __device__ __forceinline__ bool gauss_jordan(double* M, int l) {
 }
 
 // The same elimination with the augmented matrix in registers: lane j (0..16) holds column j of
-// [J | r] (m[i] = M[i][j]).  Per pivot step lane c publishes its column through LDS (one write,
-// one broadcast read: the step's only round trip), every lane finds the same pivot row and
-// multipliers M[i][c] from it, and each lane updates its own column -- the pivot-row division and
-// the elimination run across the 17 columns at once.  Same operations in the same order as
-// hg::solve16 (and as the LDS elimination above); an update the host skips (f == 0) is computed and
-// discarded here.
-// One pivot step C of the register Gauss-Jordan below (C a template parameter: every array index
-// is a compile-time constant).
+// [J | r] (m[i] = M[i][j]).  One pivot step C (a template parameter: every array index is a
+// compile-time constant): lane c's column goes to LDS while every lane searches its own column for
+// the pivot (lane c's search is the step's; the others are discarded), the multipliers M[i][c] are
+// read back with rows c and p already exchanged in the addressing while each lane swaps the two rows
+// of its own column, and then each lane divides and eliminates its own column -- the LDS round trip
+// hides behind the search and the swap.  Same operations in the same order as hg::solve16 (and as
+// the LDS elimination above); an update the host skips (f == 0) is computed and discarded here.
 template <int C>
 __device__ __forceinline__ bool gj_step(double (&m)[16], double* colbuf, int l, bool stamp) {
     constexpr int c = C;
@@ -141,18 +140,23 @@ __device__ __forceinline__ bool gj_step(double (&m)[16], double* colbuf, int l, 
 #pragma unroll
         for (int i = 0; i < 16; ++i) colbuf[i] = m[i];
     }
-    lds_order();
-    double f[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) f[i] = colbuf[i];
-    lds_order();   // read before the next step's column is written
-    GJSTAMP(1, "v"(f[15]));
-    int p = c;     // first row of maximal |M[i][c]| among rows c..15 (strict >, as the host)
-    double mx = f[c];
+    int pl = c;    // first row of maximal |M[i][c]| among rows c..15 (strict >, as the host)
+    double mxl = m[c];
 #pragma unroll
     for (int i = c + 1; i < 16; ++i)
-        if (fabs(f[i]) > fabs(mx)) { p = i; mx = f[i]; }
-    p = __builtin_amdgcn_readfirstlane(p);   // the same in every lane
+        if (fabs(m[i]) > fabs(mxl)) { pl = i; mxl = m[i]; }
+    const int p = __builtin_amdgcn_readlane(pl, c);
+    const double mp = read_lane(mxl, c);        // the pivot M[p][c]
+    GJSTAMP(1, "s"(p));
+    if (__builtin_amdgcn_readfirstlane((int)(mp == 0.0 || !isfinite(mp)))) return false;
+    lds_order();
+    double f[16];                                // M[i][c] after the row exchange (f[c] unused)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i == c) continue;
+        f[i] = i < c ? colbuf[i] : colbuf[i == p ? c : i];
+    }
+    lds_order();   // read before the next step's column is written
     GJSTAMP(2, "s"(p));
     if (p != c) {   // uniform: rows c and p swap in every column (one scalar branch per row; a
                     // binary tree of branches put the arrays in scratch memory)
@@ -160,16 +164,11 @@ __device__ __forceinline__ bool gj_step(double (&m)[16], double* colbuf, int l, 
         for (int i = c + 1; i < 16; ++i)
             if (p == i) {
                 asm volatile("" ::: "memory");   // a branch, not 8 selects per row
-                double t = m[c];
+                const double t = m[c];
                 m[c] = m[i];
                 m[i] = t;
-                t = f[c];
-                f[c] = f[i];
-                f[i] = t;
             }
     }
-    const double mp = f[c];                     // the pivot, after the swap
-    if (__builtin_amdgcn_readfirstlane((int)(mp == 0.0 || !isfinite(mp)))) return false;
     GJSTAMP(3, "v"(m[c]));
     const bool upd = l < 17 && l >= c;   // columns j >= c
     const double piv = m[c] / mp;
@@ -184,7 +183,6 @@ __device__ __forceinline__ bool gj_step(double (&m)[16], double* colbuf, int l, 
     GJSTAMP(5, "v"(m[0]), "v"(m[15]));
     return true;
 }
-
 template <int C>
 __device__ __forceinline__ bool gj_steps(double (&m)[16], double* colbuf, int l, bool stamp) {
     if (!gj_step<C>(m, colbuf, l, stamp)) return false;
@@ -192,13 +190,7 @@ __device__ __forceinline__ bool gj_steps(double (&m)[16], double* colbuf, int l,
     return true;
 }
 
-// The same elimination with the augmented matrix in registers: lane j (0..16) holds column j of
-// [J | r] (m[i] = M[i][j]).  Per pivot step lane c publishes its column through LDS (one write,
-// one broadcast read: the step's only round trip), every lane finds the same pivot row and
-// multipliers M[i][c] from it, and each lane updates its own column -- the pivot-row division and
-// the elimination run across the 17 columns at once.  Same operations in the same order as
-// hg::solve16 (and as the LDS elimination above); an update the host skips (f == 0) is computed and
-// discarded here.
+// The 16 pivot steps of the register elimination.
 __device__ __forceinline__ bool gauss_jordan_cols(double (&m)[16], double* colbuf, int l, bool stamp) {
     return gj_steps<0>(m, colbuf, l, stamp);
 }

@@ -33,7 +33,8 @@ def main():
         gj = (t[4 + 4 * r] - t[3 + 4 * r]) / ghz / 1e3
         print(f"round {r}: eval {e:6.2f} us  accept+columns {acc:6.2f} us  gauss-jordan {gj:6.2f} us")
         r += 1
-    names = ["publish+read column (LDS)", "pivot search", "row swap", "pivot division", "elimination"]
+    names = ["column publish + pivot search", "multiplier reads (issue)", "row swap (+ LDS wait)",
+             "pivot division", "elimination"]
     for c in range(2):
         s = t[40 + 6 * c: 46 + 6 * c]
         if np.all(s > 0):
