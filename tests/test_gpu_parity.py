@@ -430,6 +430,53 @@ def test_ragged_batch_sizes(torch, n):
     env.close()
 
 
+@pytest.mark.parametrize("n", [1, 200, 4161])
+def test_reset_count_across_consecutive_launches(torch, n):
+    """The reset compaction's count and the re-trim queue start from zero in every launch: over
+    consecutive eager and graph-replayed steps with resets in every step (staggered TimeLimit),
+    each step's count and index set equal its done flags; with auto-reset off a passed count
+    reads 0."""
+    import ctypes
+    from heligym_amd.vector import _ptr
+    for mode in ("template", "retrim"):
+        env = make_env(torch, n, "hover", 0.01, autoreset=True, max_episode_steps=3, reset_mode=mode)
+        env.reset()
+        st, ctr = env.get_state()
+        ctr[:, 0] = torch.arange(n, device=env.device, dtype=torch.int32) % 3
+        env.set_state(st, ctr)
+        act = torch.zeros((n, 4), device=env.device)
+        for _ in range(7):
+            obs, rew, term, trunc, info = env.step(act)
+            done = (term | trunc).cpu().numpy()
+            assert int(env.reset_count.item()) == done.sum()
+            np.testing.assert_array_equal(info["reset_index"].cpu().numpy(), np.nonzero(done)[0])
+        assert env.retrim_failures() == 0
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            env.step_async(act)
+            env.step_async(act)   # an even count: the replays keep the info buffers' alternation
+        cnt_t, idx_t = env.reset_count, env.reset_index
+        for _ in range(3):
+            g.replay()
+            torch.cuda.synchronize()
+            done = (env.terminated_u8 | env.truncated_u8).cpu().numpy()
+            k = int(cnt_t.item())
+            assert k == done.sum(), mode
+            np.testing.assert_array_equal(np.sort(idx_t[:k].cpu().numpy()), np.nonzero(done)[0])
+        env.close()
+    env = make_env(torch, n, "hover", 0.01, autoreset=False)
+    env.reset()
+    cnt = torch.full((1,), 7, dtype=torch.int32, device=env.device)
+    act = torch.zeros((n, 4), device=env.device)
+    for _ in range(2):
+        env._check(env.lib.hg_step(env._h, _ptr(act), _ptr(env.obs), _ptr(env.reward), _ptr(env.terminated_u8),
+                                   _ptr(env.truncated_u8), None, None, _ptr(cnt), None, None,
+                                   ctypes.c_void_p(torch.cuda.current_stream(env.device).cuda_stream)))
+        assert int(cnt.item()) == 0
+        cnt.fill_(7)
+    env.close()
+
+
 def test_setters_match_reference_semantics(torch, terrain_u16):
     """set_trim_cond / set_target / set_max_time (helicopter.py:89-106) through the batched env:
     the reset state is the re-trimmed one, the reward uses the new target, and `truncated` rises on
