@@ -124,12 +124,12 @@ __device__ __forceinline__ bool gauss_jordan(double* M, int l) {
 }
 
 // The same elimination with the augmented matrix in registers: lane j (0..16) holds column j of
-// [J | r] (m[i] = M[i][j]).  One pivot step C (a template parameter: every array index is a
+// [J | r] (m[i] = M[i][j]).  One pivot step C (a template parameter: every other array index is a
 // compile-time constant): lane c's column goes to LDS while every lane searches its own column for
 // the pivot (lane c's search is the step's; the others are discarded), the multipliers M[i][c] are
-// read back with rows c and p already exchanged in the addressing while each lane swaps the two rows
-// of its own column, and then each lane divides and eliminates its own column -- the LDS round trip
-// hides behind the search and the swap.  Same operations in the same order as hg::solve16 (and as
+// read back with rows c and p already exchanged in the addressing while each lane swaps the two
+// rows of its own column (a register-indexed move), and then each lane divides and eliminates its
+// own column -- the LDS round trip hides behind the search and the swap.  Same operations in the same order as hg::solve16 (and as
 // the LDS elimination above); an update the host skips (f == 0) is computed and discarded here.
 template <int C>
 __device__ __forceinline__ bool gj_step(double (&m)[16], double* colbuf, int l, bool stamp) {
@@ -158,16 +158,12 @@ __device__ __forceinline__ bool gj_step(double (&m)[16], double* colbuf, int l, 
     }
     lds_order();   // read before the next step's column is written
     GJSTAMP(2, "s"(p));
-    if (p != c) {   // uniform: rows c and p swap in every column (one scalar branch per row; a
-                    // binary tree of branches put the arrays in scratch memory)
-#pragma unroll
-        for (int i = c + 1; i < 16; ++i)
-            if (p == i) {
-                asm volatile("" ::: "memory");   // a branch, not 8 selects per row
-                const double t = m[c];
-                m[c] = m[i];
-                m[i] = t;
-            }
+    {   // rows c and p exchange in every column: p is uniform, so this is a register-indexed move
+        // (s_set_gpr_idx), not the 15 scalar branches of a test per row (one branch per row cost
+        // 5 % more; a binary tree of branches put the arrays in scratch memory)
+        const double t = m[p];
+        m[p] = m[c];
+        m[c] = t;
     }
     GJSTAMP(3, "v"(m[c]));
     const bool upd = l < 17 && l >= c;   // columns j >= c
