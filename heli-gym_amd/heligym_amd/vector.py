@@ -45,18 +45,20 @@ class LazyInfo(dict):
     a field after they were reused raises instead of returning another step's data."""
 
     def __init__(self, thunks, valid):
-        super().__init__({k: None for k in thunks})
-        self._thunks = dict(thunks)
+        """thunks: key -> f(info) computing the value (shared between steps: per-step state goes
+        on the info object); valid: () -> bool."""
+        super().__init__(dict.fromkeys(thunks))
+        self._thunks = thunks
+        self._pending = set(thunks)
         self._valid = valid
 
     def _get(self, k):
-        th = self._thunks.get(k)
-        if th is not None:
+        if k in self._pending:
             if not self._valid():
                 raise _abi.HeliGymError(f"info[{k!r}] read after its buffers were reused (read info before "
                                         "the step after next)")
-            dict.__setitem__(self, k, th())
-            del self._thunks[k]
+            dict.__setitem__(self, k, self._thunks[k](self))
+            self._pending.discard(k)
         return dict.__getitem__(self, k)
 
     def __getitem__(self, k):
@@ -169,6 +171,17 @@ class HeliVecEnv(*_VEC_BASES):
                            count=torch.zeros((1,), dtype=i32, device=dev),
                            index=torch.empty((N,), dtype=i32, device=dev),
                            final=torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)) for _ in range(2)]
+        # the per-step host path passes plain addresses (no per-call tensor -> pointer conversions)
+        # and reads the current stream through torch's raw-stream accessor
+        self._dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
+        self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        self._p_obs, self._p_rew = self.obs.data_ptr(), self.reward.data_ptr()
+        self._p_term, self._p_trunc = self.terminated_u8.data_ptr(), self.truncated_u8.data_ptr()
+        self._term_b, self._trunc_b = self.terminated_u8.view(torch.bool), self.truncated_u8.view(torch.bool)
+        self._act_shape = (N, _abi.HG_N_ACT)
+        for b in self._sets:
+            b["p"] = tuple(b[k].data_ptr() for k in ("info", "count", "index", "final"))
+            b["thunks"] = self._info_thunks(b)
         self._gen = 0
         self._use_set(0)
         # gymnasium.vector's convention: one env's spaces (helicopter.py:56-57) and the batched ones
@@ -187,9 +200,32 @@ class HeliVecEnv(*_VEC_BASES):
     def _use_set(self, g):
         b = self._sets[g & 1]
         self.info_u8, self.reset_count, self.reset_index, self.final_obs = b["info"], b["count"], b["index"], b["final"]
+        return b
 
     def _stream(self):
+        if self._raw_stream is not None:
+            return ctypes.c_void_p(self._raw_stream(self._dev_index))
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _info_thunks(self, b):
+        """The lazy info fields of a step that used buffer set b: key -> f(info)."""
+        bits, cnt, index, final = b["info"], b["count"], b["index"], b["final"]
+        th = {"failed": lambda i: (bits & _abi.HG_INFO_FAILED) != 0,
+              "successed": lambda i: (bits & _abi.HG_INFO_SUCCESSED) != 0,
+              "time_up": lambda i: (bits & _abi.HG_INFO_TIME_UP) != 0,
+              "success_step": lambda i: (bits & _abi.HG_INFO_SUCCESS_STEP) != 0}
+        if self.autoreset and self.autoreset_mode == "same_step":
+            def resets(i):   # (sorted env ids, their terminal observations); one host read per step
+                r = getattr(i, "_resets", None)
+                if r is None:
+                    k = int(cnt.item())
+                    idx = index[:k].long()
+                    order = self.torch.argsort(idx)
+                    r = i._resets = (idx[order], final[:k][order])
+                return r
+            th["reset_index"] = lambda i: resets(i)[0]
+            th["final_obs"] = lambda i: resets(i)[1]
+        return th
 
     def _check(self, rc):
         return _abi.check(rc, self.lib)
@@ -226,59 +262,47 @@ class HeliVecEnv(*_VEC_BASES):
         (already scaled by 1/sqrt(dt)), else in-kernel Philox.  obs_out: optional float32 [N,17]
         device tensor (16-byte aligned) the observations go to instead of `self.obs` (double
         buffering, e.g. while a previous step's observations are being gathered)."""
+        self._launch(actions, eta, with_reset_info, obs_out)
+
+    def _launch(self, actions, eta, with_reset_info, obs_out):
+        """step_async's launch; returns the buffer set the step's info went to."""
         a = actions
         if a.dtype != self.torch.float32 or not a.is_contiguous() or a.device != self.device:
             a = a.to(device=self.device, dtype=self.torch.float32).contiguous()
-        if tuple(a.shape) != (self.num_envs, _abi.HG_N_ACT):
+        if a.shape != self._act_shape:
             raise ValueError(f"actions must be [{self.num_envs}, 4], got {tuple(a.shape)}")
         e = None
         if eta is not None:
             e = eta.to(device=self.device, dtype=self.torch.float32).contiguous()
             if tuple(e.shape) != (self.num_envs, 3):
                 raise ValueError("eta must be [N, 3]")
-        o = self.obs
+        p_obs = self._p_obs
         if obs_out is not None:
             if (obs_out.dtype != self.torch.float32 or obs_out.device != self.device or not obs_out.is_contiguous()
                     or tuple(obs_out.shape) != (self.num_envs, _abi.HG_N_OBS)):
                 raise ValueError(f"obs_out must be a contiguous float32 [{self.num_envs}, 17] tensor on {self.device}")
-            o = obs_out
-        self._keep = (a, e, o)
+            p_obs = obs_out.data_ptr()
+        self._keep = (a, e, obs_out)
         self._gen += 1
-        self._use_set(self._gen)
+        b = self._use_set(self._gen)
+        p = b["p"]
         rs = with_reset_info and self.autoreset and self.autoreset_mode == "same_step"
-        self._check(self.lib.hg_step(
-            self._h, _ptr(a), _ptr(o), _ptr(self.reward), _ptr(self.terminated_u8),
-            _ptr(self.truncated_u8), _ptr(self.info_u8), _ptr(e),
-            _ptr(self.reset_count) if rs else None, _ptr(self.reset_index) if rs else None,
-            _ptr(self.final_obs) if rs else None, self._stream()))
+        rc = self.lib.hg_step(self._h, a.data_ptr(), p_obs, self._p_rew, self._p_term, self._p_trunc, p[0],
+                              None if e is None else e.data_ptr(), p[1] if rs else None, p[2] if rs else None,
+                              p[3] if rs else None, self._stream())
+        if rc:
+            self._check(rc)
+        return b
 
     def step(self, actions, eta=None):
         """Heli.step (helicopter.py:192-206) for all envs: (obs, reward, terminated, truncated, info).
         Returned tensors are the env's buffers, overwritten by the next step.  `info` is evaluated
         lazily: a field costs its device ops (and, for the same-step reset info, a read of the reset
         count) only when it is read, which must happen before the step after next."""
-        self.step_async(actions, eta)
-        t = self.torch
-        gen, bits = self._gen, self.info_u8
-        th = {"failed": lambda: (bits & _abi.HG_INFO_FAILED) != 0,
-              "successed": lambda: (bits & _abi.HG_INFO_SUCCESSED) != 0,
-              "time_up": lambda: (bits & _abi.HG_INFO_TIME_UP) != 0,
-              "success_step": lambda: (bits & _abi.HG_INFO_SUCCESS_STEP) != 0}
-        if self.autoreset and self.autoreset_mode == "same_step":
-            cnt, index, final = self.reset_count, self.reset_index, self.final_obs
-            cache = {}
-
-            def resets():   # (sorted env ids, their terminal observations); one host read
-                if "r" not in cache:
-                    k = int(cnt.item())
-                    idx = index[:k].long()
-                    order = t.argsort(idx)
-                    cache["r"] = (idx[order], final[:k][order])
-                return cache["r"]
-            th["reset_index"] = lambda: resets()[0]
-            th["final_obs"] = lambda: resets()[1]
-        info = LazyInfo(th, lambda: self._gen - gen < 2)
-        return self.obs, self.reward, self.terminated_u8.view(t.bool), self.truncated_u8.view(t.bool), info
+        b = self._launch(actions, eta, True, None)
+        gen = self._gen
+        info = LazyInfo(b["thunks"], lambda: self._gen - gen < 2)
+        return self.obs, self.reward, self._term_b, self._trunc_b, info
 
     # ------------------------------------------------------------------ setters (helicopter.py:89-111)
     def set_max_time(self, max_time=None):
