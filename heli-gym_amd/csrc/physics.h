@@ -591,6 +591,13 @@ HD Loads<R> main_loads(const Params<R>& P, const R* __restrict__ s, const Contro
     const R Y_F = rh * P.fus_YVV * m_fabs(va) * va;
     const R Z_F = rh * P.fus_ZWW * m_fabs(wa_f) * wa_f;
     const R power_fus = -X_F * ua - Y_F * va - Z_F * wa_f;
+    // Z_F * d_fw -> 0 as wa_f -> 0 (Z_F ~ wa_f^2, d_fw ~ 1/wa_f).  At wa_f == 0 exactly the reference's
+    // expression is 0 * inf = NaN; in its fp64 arithmetic that point is never hit, while this fp32
+    // restatement lands on it about once per 1e9 stage evaluations (a descending helicopter with
+    // w_air == vi_mr), which would leave the env NaN until its time limit.  The fp32 step takes the
+    // limit there; the fp64 trims keep the reference's expression.
+    R zd = Z_F * d_fw;
+    if constexpr (sizeof(R) == sizeof(float)) zd = wa_f == (R)0 ? (R)0 : zd;
     // climb and fuselage power load the main rotor's torque (:446-447)
     const R power_climb = P.wt * (-f.n2);
     const R p_extra = power_climb + power_fus;
@@ -598,7 +605,7 @@ HD Loads<R> main_loads(const Params<R>& P, const R* __restrict__ s, const Contro
     o.F[1] = Y_MR + Y_F;
     o.F[2] = Z_MR + Z_F;
     o.M[0] = L_MR + Y_F * P.fus_H;
-    o.M[1] = M_MR + (Z_F * d_fw - X_F * P.fus_H);
+    o.M[1] = M_MR + (zd - X_F * P.fus_H);
     o.M[2] = power_mr * P.mr_inv_OMEGA + p_extra * P.mr_inv_OMEGA;
     o.power = power_mr + p_extra;
     return o;
