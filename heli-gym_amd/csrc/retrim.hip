@@ -42,8 +42,8 @@ __device__ unsigned long long g_rt_timing[64];
 // reset_mode RETRIM (F8) and hg_trim_batch.  One wave per trim, fp64 throughout, every lane holding
 // the same Newton iterate:
 //   * lanes 0..15 / 16..31 evaluate the +eps / -eps Jacobian columns in parallel;
-//   * lane j <= 16 then holds column j of [J | r] in registers and the Gauss-Jordan elimination
-//     (hg::solve16, same operation order) runs with the pivot column broadcast by readlane;
+//   * the Gauss-Jordan elimination of [J | r] (hg::solve16, same operation order) runs over the
+//     whole wave, four lanes per row (gauss_jordan_wave);
 //   * lanes 0..9 evaluate the ten step-halving trials at once; the first one that lowers the
 //     residual is the trial the reference's sequential search accepts.
 
@@ -61,13 +61,24 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// hg::solve16 (np.linalg.inv(dydx) @ r, helicopter_dynamics.py:524-527) on the augmented matrix
-// [J | r] (16 x 17 doubles, row-major) in LDS: Gauss-Jordan with partial pivoting in the host
-// solver's operation order.  Every lane reads the pivot column (broadcast reads) and finds the
-// pivot itself; lane e owns the elements e, e + 64, ... of the elimination, whose operands (the
-// row's multiplier and the pivot row's element) are all read before any element is written.
-constexpr int kGJElems = 16 * 17;
-
+// hg::solve16 (np.linalg.inv(dydx) @ r, helicopter_dynamics.py:524-527): Gauss-Jordan with partial
+// pivoting on the augmented matrix [J | r] spread over the whole wave.  Lane l = 16 q + i holds row i
+// of columns 4q .. 4q+3 and of the right-hand side (a[0..3], a[4]; the right-hand side is kept by all
+// four lanes of a row, which compute it identically), so a DPP row of 16 lanes is one column
+// quarter.  Per pivot step C:
+//   * the pivot search is a 4-level DPP rotation reduction over the 16 rows of column C (in the
+//     row of lanes that holds it) instead of a serial scan;
+//   * rows are never moved: every row carries its position in the host's row order (`pos`, the
+//     same in its four lanes), exchanged by the pivot step as the host exchanges the rows, and the
+//     search breaks ties by that position, so the pivot is the host's (first row of maximal |M[i][C]|
+//     among positions C..15, strict >);
+//   * the multiplier M[i][C] (from the lane of this row that holds column C) and the pivot row's
+//     elements (from the lane of the pivot row that holds this lane's columns) are two ds_bpermute
+//     reads; the first is issued before the search, as it does not depend on the pivot;
+//   * each lane scales the pivot row by 1/pivot and eliminates its own five elements.
+// The values of columns >= C and of the right-hand side are the host's bit for bit (hg::solve16 in
+// the same operation order, unfused); columns < C, which the host leaves alone and never reads
+// again, are updated here too and ignored.  The solution is the right-hand side in host order.
 // The block is one wave, whose LDS operations execute in issue order: a read issued after a write
 // sees it.  This only keeps the compiler from reordering LDS accesses across the point (no
 // s_barrier, no wait for the LDS queue to drain).
@@ -75,125 +86,88 @@ __device__ __forceinline__ void lds_order() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
-constexpr int kGJPerLane = (kGJElems + 63) / 64;
 
-__device__ __forceinline__ bool gauss_jordan(double* M, int l) {
-    int ei[kGJPerLane], ej[kGJPerLane];   // row / column of this lane's elements
-#pragma unroll
-    for (int k = 0; k < kGJPerLane; ++k) {
-        ei[k] = (l + 64 * k) / 17;
-        ej[k] = (l + 64 * k) - 17 * ei[k];
+__device__ __forceinline__ int ror16(int v, int n) {   // n: compile-time after inlining
+    switch (n) {
+        case 8: return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);
+        case 4: return __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);
+        case 2: return __builtin_amdgcn_update_dpp(0, v, 0x122, 0xF, 0xF, false);
+        default: return __builtin_amdgcn_update_dpp(0, v, 0x121, 0xF, 0xF, false);
     }
-#pragma unroll
-    for (int c = 0; c < 16; ++c) {
-        int p = c;   // first row of maximal |M[i][c]| among rows c..15 (strict >, as the host)
-        double mp = M[c * 17 + c];
-#pragma unroll
-        for (int i = c + 1; i < 16; ++i) {
-            const double v = M[i * 17 + c];
-            if (fabs(v) > fabs(mp)) { p = i; mp = v; }
-        }
-        if (mp == 0.0 || !isfinite(mp)) return false;
-        if (p != c) {   // wave-uniform
-            lds_order();
-            if (l < 17) {
-                const double t = M[c * 17 + l];
-                M[c * 17 + l] = M[p * 17 + l];
-                M[p * 17 + l] = t;
-            }
-        }
-        lds_order();
-        if (l >= c && l < 17) M[c * 17 + l] /= mp;   // the pivot row, j >= c
-        lds_order();
-        double f[kGJPerLane], pr[kGJPerLane];
-#pragma unroll
-        for (int k = 0; k < kGJPerLane; ++k) {
-            const bool in = l + 64 * k < kGJElems;
-            f[k] = in ? M[ei[k] * 17 + c] : 0.0;
-            pr[k] = in ? M[c * 17 + ej[k]] : 0.0;
-        }
-        lds_order();
-#pragma unroll
-        for (int k = 0; k < kGJPerLane; ++k) {
-            const int e = l + 64 * k;
-            if (e < kGJElems && ei[k] != c && ej[k] >= c && f[k] != 0.0) M[e] -= f[k] * pr[k];
-        }
-        lds_order();
-    }
-    return true;
 }
 
-// The same elimination with the augmented matrix in registers: lane j (0..16) holds column j of
-// [J | r] (m[i] = M[i][j]).  One pivot step C (a template parameter: every other array index is a
-// compile-time constant): lane c's column goes to LDS while every lane searches its own column for
-// the pivot (lane c's search is the step's; the others are discarded), the multipliers M[i][c] are
-// read back with rows c and p already exchanged in the addressing while each lane swaps the two
-// rows of its own column (a register-indexed move), and then each lane divides and eliminates its
-// own column -- the LDS round trip hides behind the search and the swap.  Same operations in the same order as hg::solve16 (and as
-// the LDS elimination above); an update the host skips (f == 0) is computed and discarded here.
 template <int C>
-__device__ __forceinline__ bool gj_step(double (&m)[16], double* colbuf, int l, bool stamp) {
-    constexpr int c = C;
+__device__ __forceinline__ bool gj_step(double (&a)[5], int& pos, int l, bool stamp) {
+    constexpr int c = C, qc = C >> 2, tc = C & 3;
     (void)stamp;
-    GJSTAMP(0, "v"(m[0]));
-    if (l == c) {
+    (void)c;
+    const int i = l & 15, q = l >> 4;
+    GJSTAMP(0, "v"(a[0]));
+    const double f = shfl_d(a[tc], 16 * qc + i);   // M[i][C] of this lane's row
+    const double v = a[tc];                         // M[i][4q + tc]; row of lanes qc: column C
+    const bool nan_v = v != v;
+    uint64_t key = (pos >= C && !nan_v) ? (uint64_t)__double_as_longlong(fabs(v)) + 1 : 0;
+    int id = (pos << 4) | i;                        // ties: the smallest host position
 #pragma unroll
-        for (int i = 0; i < 16; ++i) colbuf[i] = m[i];
+    for (int sh = 8; sh >= 1; sh >>= 1) {
+        const uint32_t klo = (uint32_t)ror16((int)(uint32_t)key, sh);
+        const uint32_t khi = (uint32_t)ror16((int)(uint32_t)(key >> 32), sh);
+        const uint64_t ko = ((uint64_t)khi << 32) | klo;
+        const int io = ror16(id, sh);
+        const bool take = ko > key || (ko == key && io < id);
+        key = take ? ko : key;
+        id = take ? io : id;
     }
-    int pl = c;    // first row of maximal |M[i][c]| among rows c..15 (strict >, as the host)
-    double mxl = m[c];
+    const int pid = __builtin_amdgcn_readlane(id, 16 * qc);
+    const int P = pid & 15, ppos = pid >> 4;
+    const double mp = read_lane(v, 16 * qc + P);    // the pivot M[P][C]
+    // the host's first candidate M[C][C] being NaN keeps it as the (non-finite) pivot
+    const bool c_nan = __ballot(q == qc && pos == C && nan_v) != 0;
+    GJSTAMP(1, "s"(pid));
+    if (c_nan || mp == 0.0 || !isfinite(mp)) return false;
+    const double rinv = 1.0 / mp;
+    double pr[5];
 #pragma unroll
-    for (int i = c + 1; i < 16; ++i)
-        if (fabs(m[i]) > fabs(mxl)) { pl = i; mxl = m[i]; }
-    const int p = __builtin_amdgcn_readlane(pl, c);
-    const double mp = read_lane(mxl, c);        // the pivot M[p][c]
-    GJSTAMP(1, "s"(p));
-    if (__builtin_amdgcn_readfirstlane((int)(mp == 0.0 || !isfinite(mp)))) return false;
-    lds_order();
-    double f[16];                                // M[i][c] after the row exchange (f[c] unused)
+    for (int t = 0; t < 5; ++t) pr[t] = shfl_d(a[t], 16 * q + P) * rinv;   // pivot row / pivot
+    GJSTAMP(2, "v"(pr[0]), "v"(pr[4]));
+    const bool is_piv = i == P;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if (i == c) continue;
-        f[i] = i < c ? colbuf[i] : colbuf[i == p ? c : i];
+    for (int t = 0; t < 5; ++t) {
+        const double u = a[t] - f * pr[t];
+        a[t] = is_piv ? pr[t] : (f != 0.0 ? u : a[t]);
     }
-    lds_order();   // read before the next step's column is written
-    GJSTAMP(2, "s"(p));
-    {   // rows c and p exchange in every column: p is uniform, so this is a register-indexed move
-        // (s_set_gpr_idx), not the 15 scalar branches of a test per row (one branch per row cost
-        // 5 % more; a binary tree of branches put the arrays in scratch memory)
-        const double t = m[p];
-        m[p] = m[c];
-        m[c] = t;
-    }
-    GJSTAMP(3, "v"(m[c]));
-    const bool upd = l < 17 && l >= c;   // columns j >= c
-    const double piv = m[c] / mp;
-    m[c] = upd ? piv : m[c];
-    GJSTAMP(4, "v"(m[c]));
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        if (i == c) continue;
-        const double t = m[i] - f[i] * m[c];
-        m[i] = (upd && f[i] != 0.0) ? t : m[i];
-    }
-    GJSTAMP(5, "v"(m[0]), "v"(m[15]));
+    pos = pos == ppos ? C : (pos == C ? ppos : pos);
+    GJSTAMP(3, "v"(a[0]), "v"(a[4]));
     return true;
 }
 template <int C>
-__device__ __forceinline__ bool gj_steps(double (&m)[16], double* colbuf, int l, bool stamp) {
-    if (!gj_step<C>(m, colbuf, l, stamp)) return false;
-    if constexpr (C < 15) return gj_steps<C + 1>(m, colbuf, l, stamp);
+__device__ __forceinline__ bool gj_steps(double (&a)[5], int& pos, int l, bool stamp) {
+    if (!gj_step<C>(a, pos, l, stamp)) return false;
+    if constexpr (C < 15) return gj_steps<C + 1>(a, pos, l, stamp);
     return true;
 }
 
-// The 16 pivot steps of the register elimination.
-__device__ __forceinline__ bool gauss_jordan_cols(double (&m)[16], double* colbuf, int l, bool stamp) {
-    return gj_steps<0>(m, colbuf, l, stamp);
+// The Newton system arrives in LDS as the raw evaluations: E[j][k] = y_k at x + eps e_j (j < 16) and
+// at x - eps e_{j-16} (16 <= j < 32), R[k] = y_k - y*_k.  Each lane forms its own four Jacobian
+// elements (J[i][j] = (E[j][i] - E[j+16][i]) / (2 eps), helicopter_dynamics.py:521-523, the host's
+// operation) and right-hand side, so the 256 divisions are spread over the wave (4 per lane); the
+// solution leaves through `sol` in host row order.
+__device__ __forceinline__ bool gauss_jordan_wave(const double* E, const double* R, double* sol, int l, bool stamp,
+                                                  double (&dir)[16]) {
+    const int i = l & 15, q = l >> 4;
+    const double eps = hg::kTrimEps;
+    double a[5];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a[t] = (E[(4 * q + t) * 16 + i] - E[(4 * q + t + 16) * 16 + i]) / (2 * eps);
+    a[4] = R[i];
+    int pos = i;
+    if (!gj_steps<0>(a, pos, l, stamp)) return false;
+    if (l < 16) sol[pos] = a[4];
+    lds_order();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dir[k] = sol[k];
+    return true;
 }
-
-#ifndef HG_GJ_LDS
-#define HG_GJ_LDS 0   // 1: the LDS elimination (A/B)
-#endif
 
 __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, int64_t env, const double x[16],
                                              const double s[18], const double ob[17]) {
@@ -220,11 +194,9 @@ __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, i
 // alone the residual at x0 in the first round.  A round is one trim_fcn latency; a trim of three
 // Newton steps takes four rounds.
 __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
-#if HG_GJ_LDS
-    __shared__ double M[kGJElems];   // [J | r] of the current Newton step
-#else
-    __shared__ double colbuf[16];    // the pivot column of the current elimination step
-#endif
+    __shared__ double gjE[32 * 16];   // the +-eps evaluations of the current Newton step
+    __shared__ double gjR[16];        // its right-hand side y - y*
+    __shared__ double gjS[16];        // its solution
     const int l = threadIdx.x;
     const hg::Params<double>& P = *a.P;
     const double eps = hg::kTrimEps;
@@ -239,7 +211,7 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
             W[1] = (double)wr[1];
             W[2] = (double)wr[2];
         }
-        double x[16], y[16], dir[16];
+        double x[16], dir[16];
         for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; }
         double tol = 0;
         int it = 0;
@@ -286,7 +258,6 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
                 }
             }
             if (src >= 0) {
-                for (int k = 0; k < 16; ++k) y[k] = read_lane(ye[k], src);
                 tol = read_lane(te, src);
                 if (!(tol > eps)) {   // converged: the accepting lane holds the final evaluation
                     done = true;
@@ -301,31 +272,21 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
                     hg::trim_fcn(P, T.base, xe, W, T.hc, ye, nullptr, nullptr, nullptr);
                 }
             }
-            // ---- Newton direction: lane j <= 16 holds column j of [J | r], then Gauss-Jordan
-            double mcol[16];
+            // ---- Newton direction: the evaluations and the residual (lane src holds y) into LDS,
+            // then Gauss-Jordan over the wave
+            lds_order();   // the previous solve's reads are done
+            if (l < 32) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const double ym = shfl_d(ye[k], (l + 16) & 63);
-                mcol[k] = l < 16 ? (ye[k] - ym) / (2 * eps) : y[k] - T.yt[k];
+                for (int k = 0; k < 16; ++k) gjE[l * 16 + k] = ye[k];
             }
-#if HG_GJ_LDS
+            if (l == src) {
 #pragma unroll
-            for (int k = 0; k < 16; ++k)
-                if (l < 17) M[k * 17 + l] = mcol[k];
-            __syncthreads();
+                for (int k = 0; k < 16; ++k) gjR[k] = ye[k] - T.yt[k];
+            }
+            lds_order();
             RSTAMP(3 + 4 * round, "v"(ye[0]));
-            ok = gauss_jordan(M, l);
+            ok = gauss_jordan_wave(gjE, gjR, gjS, l, job == 0 && round == 0, dir);
             if (!ok) break;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) dir[k] = M[k * 17 + 16];
-            __syncthreads();   // dir read before the next round's matrix is written
-#else
-            RSTAMP(3 + 4 * round, "v"(mcol[0]));
-            ok = gauss_jordan_cols(mcol, colbuf, l, job == 0 && round == 0);
-            if (!ok) break;
-#pragma unroll
-            for (int k = 0; k < 16; ++k) dir[k] = read_lane(mcol[k], 16);
-#endif
             RSTAMP(4 + 4 * round, "v"(dir[0]));
             ++round;
         }

@@ -90,8 +90,8 @@ HD bool solve16(double A[16][16], const double r[16], double v[16]) {
                 M[c][j] = M[p][j];
                 M[p][j] = t;
             }
-        const double piv = M[c][c];
-        for (int j = c; j < 17; ++j) M[c][j] /= piv;
+        const double rinv = 1.0 / M[c][c];   // one division per pivot step (the device's too)
+        for (int j = c; j < 17; ++j) M[c][j] *= rinv;
         for (int i = 0; i < 16; ++i) {
             if (i == c) continue;
             const double f = M[i][c];

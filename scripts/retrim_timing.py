@@ -33,10 +33,10 @@ def main():
         gj = (t[4 + 4 * r] - t[3 + 4 * r]) / ghz / 1e3
         print(f"round {r}: eval {e:6.2f} us  accept+columns {acc:6.2f} us  gauss-jordan {gj:6.2f} us")
         r += 1
-    names = ["column publish + pivot search", "multiplier reads (issue)", "row swap (+ LDS wait)",
-             "pivot division", "elimination"]
+    names = ["multiplier read + pivot search (DPP reduction) + readlanes", "pivot row read + scaling",
+             "elimination"]
     for c in range(2):
-        s = t[40 + 6 * c: 46 + 6 * c]
+        s = t[40 + 6 * c: 44 + 6 * c]
         if np.all(s > 0):
             print(f"pivot step {c}: " + ", ".join(f"{n} {(s[k + 1] - s[k]) / ghz:.0f} cyc" for k, n in enumerate(names)))
     env.close()
