@@ -66,8 +66,8 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
 // of columns 4q .. 4q+3 and of the right-hand side (a[0..3], a[4]; the right-hand side is kept by all
 // four lanes of a row, which compute it identically), so a DPP row of 16 lanes is one column
 // quarter.  Per pivot step C:
-//   * the pivot search is a 4-level DPP rotation reduction over the 16 rows of column C (in the
-//     row of lanes that holds it) instead of a serial scan;
+//   * the pivot search is a 4-level DPP rotation max over the 16 rows of column C (in the row of
+//     lanes that holds it) instead of a serial scan, and a ballot of the rows attaining it;
 //   * rows are never moved: every row carries its position in the host's row order (`pos`, the
 //     same in its four lanes), exchanged by the pivot step as the host exchanges the rows, and the
 //     search breaks ties by that position, so the pivot is the host's (first row of maximal |M[i][C]|
@@ -87,13 +87,24 @@ __device__ __forceinline__ void lds_order() {
     __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ int ror16(int v, int n) {   // n: compile-time after inlining
+// Rotate a double within each row of 16 lanes (DPP row_ror: every lane has a source, so no
+// "old" operand is needed); n is a compile-time constant after inlining.
+__device__ __forceinline__ double ror16_d(double v, int n) {
+    const uint64_t u = __double_as_longlong(v);
+    int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
     switch (n) {
-        case 8: return __builtin_amdgcn_update_dpp(0, v, 0x128, 0xF, 0xF, false);
-        case 4: return __builtin_amdgcn_update_dpp(0, v, 0x124, 0xF, 0xF, false);
-        case 2: return __builtin_amdgcn_update_dpp(0, v, 0x122, 0xF, 0xF, false);
-        default: return __builtin_amdgcn_update_dpp(0, v, 0x121, 0xF, 0xF, false);
+        case 8: lo = __builtin_amdgcn_mov_dpp(lo, 0x128, 0xF, 0xF, true); hi = __builtin_amdgcn_mov_dpp(hi, 0x128, 0xF, 0xF, true); break;
+        case 4: lo = __builtin_amdgcn_mov_dpp(lo, 0x124, 0xF, 0xF, true); hi = __builtin_amdgcn_mov_dpp(hi, 0x124, 0xF, 0xF, true); break;
+        case 2: lo = __builtin_amdgcn_mov_dpp(lo, 0x122, 0xF, 0xF, true); hi = __builtin_amdgcn_mov_dpp(hi, 0x122, 0xF, 0xF, true); break;
+        default: lo = __builtin_amdgcn_mov_dpp(lo, 0x121, 0xF, 0xF, true); hi = __builtin_amdgcn_mov_dpp(hi, 0x121, 0xF, 0xF, true); break;
     }
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+// v_max_f64 without the canonicalising maxes fmax() adds (the operands here are never NaN)
+__device__ __forceinline__ double vmax_d(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
 template <int C>
@@ -106,29 +117,34 @@ __device__ __forceinline__ bool gj_step(double (&a)[5], int& pos, int l, bool st
     const double f = shfl_d(a[tc], 16 * qc + i);   // M[i][C] of this lane's row
     const double v = a[tc];                         // M[i][4q + tc]; row of lanes qc: column C
     const bool nan_v = v != v;
-    uint64_t key = (pos >= C && !nan_v) ? (uint64_t)__double_as_longlong(fabs(v)) + 1 : 0;
-    int id = (pos << 4) | i;                        // ties: the smallest host position
+    const bool cand = pos >= C && !nan_v;
+    const double key = cand ? fabs(v) : -1.0;
+    double mx = key;                                // max |M[i][C]| over the candidate rows
 #pragma unroll
-    for (int sh = 8; sh >= 1; sh >>= 1) {
-        const uint32_t klo = (uint32_t)ror16((int)(uint32_t)key, sh);
-        const uint32_t khi = (uint32_t)ror16((int)(uint32_t)(key >> 32), sh);
-        const uint64_t ko = ((uint64_t)khi << 32) | klo;
-        const int io = ror16(id, sh);
-        const bool take = ko > key || (ko == key && io < id);
-        key = take ? ko : key;
-        id = take ? io : id;
+    for (int sh = 8; sh >= 1; sh >>= 1) mx = vmax_d(mx, ror16_d(mx, sh));
+    // the rows that attain it (usually one); ties go to the smallest host position
+    const uint32_t hit = (uint32_t)(__ballot(cand && key == mx) >> (16 * qc)) & 0xFFFFu;
+    int P = hit ? __builtin_ctz(hit) : 0;
+    int ppos = __builtin_amdgcn_readlane(pos, 16 * qc + P);
+    if (hit & (hit - 1)) {   // wave-uniform, rare
+        for (uint32_t m = hit & (hit - 1); m; m &= m - 1) {
+            const int b = __builtin_ctz(m);
+            const int pb = __builtin_amdgcn_readlane(pos, 16 * qc + b);
+            if (pb < ppos) { ppos = pb; P = b; }
+        }
     }
-    const int pid = __builtin_amdgcn_readlane(id, 16 * qc);
-    const int P = pid & 15, ppos = pid >> 4;
     const double mp = read_lane(v, 16 * qc + P);    // the pivot M[P][C]
-    // the host's first candidate M[C][C] being NaN keeps it as the (non-finite) pivot
-    const bool c_nan = __ballot(q == qc && pos == C && nan_v) != 0;
-    GJSTAMP(1, "s"(pid));
-    if (c_nan || mp == 0.0 || !isfinite(mp)) return false;
-    const double rinv = 1.0 / mp;
     double pr[5];
 #pragma unroll
-    for (int t = 0; t < 5; ++t) pr[t] = shfl_d(a[t], 16 * q + P) * rinv;   // pivot row / pivot
+    for (int t = 0; t < 5; ++t) pr[t] = shfl_d(a[t], 16 * q + P);   // the pivot row
+    // the host's first candidate M[C][C] being NaN keeps it as the (non-finite) pivot
+    const bool c_nan = __ballot(q == qc && pos == C && nan_v) != 0;
+    GJSTAMP(1, "s"(P));
+    if (!hit || c_nan || mp == 0.0 || !isfinite(mp)) return false;
+    __builtin_amdgcn_sched_barrier(0);   // the pivot-row reads are in flight during the division
+    const double rinv = 1.0 / mp;
+#pragma unroll
+    for (int t = 0; t < 5; ++t) pr[t] *= rinv;
     GJSTAMP(2, "v"(pr[0]), "v"(pr[4]));
     const bool is_piv = i == P;
 #pragma unroll
