@@ -804,6 +804,7 @@ hg::TrimSetup trim_setup(const Params<double>& P, const float2* hmap, const hg_t
     const double x0[16] = {0.05f, 0.05f, 0, 0, 0, 0, 0, 0, 0, (float)tc.yaw_rate, -0.01f, 0.01f, 0, 0, 0, 0};
     for (int i = 0; i < 16; ++i) t.x0[i] = x0[i];
     for (int i = 0; i < 3; ++i) t.x0[4 + i] = (float)tc.ned_vel[i] / (float)P.mr_VTIP;
+    hg::trim_precompute(P, t);
     return t;
 }
 
@@ -815,7 +816,7 @@ int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond&
     const double eps = hg::kTrimEps;
     double x[16], y[16];
     memcpy(x, T.x0, sizeof(x));
-    hg::trim_fcn(P, T.base, x, W, T.hc, y, nullptr, nullptr, nullptr);
+    hg::trim_fcn(P, T, x, W, y, nullptr, nullptr, nullptr);
     double tol = hg::trim_residual(y, T.yt);
     int it = 0;
     while (tol > eps) {
@@ -825,8 +826,8 @@ int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond&
             memcpy(xm, x, sizeof(x));
             xp[i] += eps;
             xm[i] -= eps;
-            hg::trim_fcn(P, T.base, xp, W, T.hc, yp, nullptr, nullptr, nullptr);
-            hg::trim_fcn(P, T.base, xm, W, T.hc, ym, nullptr, nullptr, nullptr);
+            hg::trim_fcn(P, T, xp, W, yp, nullptr, nullptr, nullptr);
+            hg::trim_fcn(P, T, xm, W, ym, nullptr, nullptr, nullptr);
             for (int k = 0; k < 16; ++k) J[k][i] = (yp[k] - ym[k]) / (2 * eps);
         }
         for (int k = 0; k < 16; ++k) r[k] = y[k] - T.yt[k];
@@ -835,7 +836,7 @@ int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond&
         int j;
         for (j = 0; j < hg::kTrimLineSearch; ++j) {
             for (int k = 0; k < 16; ++k) xn[k] = x[k] - step * dir[k];
-            hg::trim_fcn(P, T.base, xn, W, T.hc, yn, nullptr, nullptr, nullptr);
+            hg::trim_fcn(P, T, xn, W, yn, nullptr, nullptr, nullptr);
             tn = hg::trim_residual(yn, T.yt);
             step *= 0.5;
             if (tn < tol) break;
@@ -846,7 +847,7 @@ int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond&
         tol = tn;
         if (++it > hg::kTrimMaxIter) return fail(HG_E_TRIM, "Trim failed, please try a better trim condition!");
     }
-    hg::trim_fcn(P, T.base, x, W, T.hc, y, out->state, out->state_dots, out->obs);
+    hg::trim_fcn(P, T, x, W, y, out->state, out->state_dots, out->obs);
     for (int i = 0; i < 4; ++i) out->action[i] = x[12 + i];
     out->residual = tol;
     out->iterations = it;

@@ -479,9 +479,15 @@ struct Frame {
     R zh;                // z + h under the committed position
 };
 
+// ISA density at the altitude -z (helicopter_dynamics.py:160-165)
+template <typename R>
+HD R atmosphere_rho(const Params<R>& P, R z) {
+    return P.ro_sea * m_pow((R)1 + P.lapse_t0 * z, P.rho_exp);
+}
+
 template <typename R>
 HD Frame<R> frame(const Params<R>& P, const R* __restrict__ s, const R W[3], const Ground<R>& gc,
-                  const Attitude<R>& att) {
+                  const Attitude<R>& att, const R* rho_irho = nullptr) {
     const R uu = s[6], vv = s[7], ww = s[8], p = s[9], q = s[10], r = s[11];
     const R s0 = att.s[0], c0 = att.c[0], s1 = att.s[1], c1 = att.c[1], s2 = att.s[2], c2 = att.c[2];
     Frame<R> f;
@@ -534,8 +540,13 @@ HD Frame<R> frame(const Params<R>& P, const R* __restrict__ s, const R W[3], con
         f.va = vv - yz.x;
         f.wa = ww - yz.y;
     }
-    f.rho = P.ro_sea * m_pow((R)1 + P.lapse_t0 * s[17], P.rho_exp);
-    f.irho = m_rcp(f.rho);
+    if (rho_irho) {   // the trims: the altitude is fixed, so the density is evaluated once per trim
+        f.rho = rho_irho[0];
+        f.irho = rho_irho[1];
+    } else {
+        f.rho = atmosphere_rho(P, s[17]);
+        f.irho = m_rcp(f.rho);
+    }
     // z + h with the large cancellation first (Ground::zh): the stiff gear spring K * (pos_z + h)
     // keeps its precision near the ground
     f.zh = gc.zh(s[17]);
@@ -734,8 +745,9 @@ HD void observe(const Params<R>& P, const R* __restrict__ s, const Frame<R>& f, 
 // One evaluation of the model; with OBS also the 17 observations.
 template <bool OBS, typename R>
 HD void dynamics(const Params<R>& P, const R* __restrict__ s, const Controls<R>& u, const R W[3],
-                 const Ground<R>& gc, const Attitude<R>& att, R* __restrict__ d, R* __restrict__ obs) {
-    const Frame<R> f = frame(P, s, W, gc, att);
+                 const Ground<R>& gc, const Attitude<R>& att, R* __restrict__ d, R* __restrict__ obs,
+                 const R* rho_irho = nullptr) {
+    const Frame<R> f = frame(P, s, W, gc, att, rho_irho);
     const Loads<R> A = main_loads(P, s, u, f);
     const Loads<R> B = tail_loads(P, s, u, f);
     eom(P, s, f, A, B, d);

@@ -250,7 +250,7 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
             }
             double ye[16], se[18], de[18], oe[17];
             RSTAMP(1 + 4 * round, "v"(xe[0]));
-            hg::trim_fcn(P, T.base, xe, W, T.hc, ye, se, de, oe);
+            hg::trim_fcn(P, T, xe, W, ye, se, de, oe);
             const double te = hg::trim_residual(ye, T.yt);
             RSTAMP(2 + 4 * round, "v"(te));
             // ---- accept a trial (or take the base point)
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
             if (!have_jac) {   // the search accepted a shorter step: Jacobian at the new x
                 if (l < 32) {
                     for (int k = 0; k < 16; ++k) xe[k] = k == c ? (l < 16 ? x[k] + eps : x[k] - eps) : x[k];
-                    hg::trim_fcn(P, T.base, xe, W, T.hc, ye, nullptr, nullptr, nullptr);
+                    hg::trim_fcn(P, T, xe, W, ye, nullptr, nullptr, nullptr);
                 }
             }
             // ---- Newton direction: the evaluations and the residual (lane src holds y) into LDS,
@@ -312,7 +312,7 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
             bool written = !(tol > eps);
             if (!written) {
                 double yy[16], s[18], d[18], ob[17];
-                hg::trim_fcn(P, T.base, x, W, T.hc, yy, s, d, ob);
+                hg::trim_fcn(P, T, x, W, yy, s, d, ob);
                 retrim_write(a, job, env, x, s, ob);
             }
         }

@@ -21,7 +21,18 @@ struct TrimSetup {
     double yt[16];       // target normalised derivatives: yaw rate and ned velocity / R (:508-512)
     double x0[16];       // initial guess (:513-516)
     Ground<double> hc;   // ground under the trim position (committed xy)
+    // functions of the fixed entries alone, evaluated once per trim condition (trim_precompute):
+    double rho_irho[2];  // density at the trim altitude and its reciprocal
+    double s_psi, c_psi; // sin / cos of the fixed yaw
 };
+
+// The per-condition constants of TrimSetup, from its base state (the same functions the model
+// would evaluate on every trial point).
+HD void trim_precompute(const Params<double>& P, TrimSetup& t) {
+    t.rho_irho[0] = atmosphere_rho(P, t.base[17]);
+    t.rho_irho[1] = m_rcp(t.rho_irho[0]);
+    m_sincos(t.base[14], &t.s_psi, &t.c_psi);
+}
 
 // Trial state for the unknowns x = [vi_mr/Vtip, vi_tr/Vtip_tr, b0, b1, uvw/Vtip, pqr/Omega,
 // phi, theta, a0..a3] (:557-566), rounded to float like the reference's float32 state.
@@ -41,12 +52,17 @@ HD void trim_state(const Params<double>& P, const double base[18], const double 
 
 // __trim_fcn (:557-576): normalised derivatives y(x) at the trial point; optionally the trial
 // state, its derivatives and the observation (the final evaluation gives the reset state).
-HD void trim_fcn(const Params<double>& P, const double base[18], const double x[16], const double W[3],
-                 const Ground<double>& hc, double y[16], double* s_out, double* d_out, double* obs) {
+HD void trim_fcn(const Params<double>& P, const TrimSetup& T, const double x[16], const double W[3],
+                 double y[16], double* s_out, double* d_out, double* obs) {
     double s[18], d[18], ob[17];
-    trim_state(P, base, x, s);
+    trim_state(P, T.base, x, s);
     const Controls<double> u = controls(P, x[12], x[13], x[14], x[15]);
-    dynamics<true>(P, s, u, W, hc, attitude(s + 12), d, ob);
+    Attitude<double> att;   // phi, theta are trial values; the yaw is fixed
+    m_sincos(s[12], &att.s[0], &att.c[0]);
+    m_sincos(s[13], &att.s[1], &att.c[1]);
+    att.s[2] = T.s_psi;
+    att.c[2] = T.c_psi;
+    dynamics<true>(P, s, u, W, T.hc, att, d, ob, T.rho_irho);
     y[0] = d[0] / P.mr_VTIP;
     y[1] = d[1] / P.tr_VTIP;
     y[2] = d[4];
