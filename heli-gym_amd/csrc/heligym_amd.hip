@@ -97,6 +97,7 @@ struct StepArgs {
     uint8_t* info;
     const float* eta;
     int32_t* reset_count;
+    int32_t* reset_count_next;   // FEAT: zeroed by this launch for a later step (hg_step_chained), or NULL
     int32_t* reset_index;
     float* final_obs;
     float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
@@ -342,6 +343,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
 #pragma unroll
     for (int c = 0; c < 18; ++c)   // ... and the heli state streams in behind the noise and wind work
         if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lt);
+    if (FEAT && a.reset_count_next && blockIdx.x == 0 && tid == 0) *a.reset_count_next = 0;
     const int nsteps = MULTI ? a.nsteps : 1;
     for (int sstep = 0; sstep < nsteps; ++sstep) {
     // MULTI: the constants are re-read (scalar cache) each step rather than kept live across the
@@ -902,6 +904,7 @@ struct hg_env {
     bool baked = false;                     // step with the constant-specialised kernel (baked.h)
     bool baked_allowed = true;              // ... unless switched off (hg_set_specialized)
     hg::TrimSetup* setup_batch = nullptr;   // hg_trim_conds_batch scratch
+    bool chain_after_capture = true;        // hg_step_chained: re-zero the count (first call, after a capture)
     int64_t setup_batch_cap = 0;
 };
 
@@ -1243,9 +1246,9 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
     return HG_OK;
 }
 
-int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint8_t* terminated,
-                uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count, int32_t* reset_index,
-                float* final_obs, void* stream) {
+static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                         uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count,
+                         int32_t* reset_index, float* final_obs, int32_t* reset_count_next, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
@@ -1255,8 +1258,20 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
         return fail(HG_E_INVALID, "actions and obs must be 16-byte aligned");
     if ((reset_index || final_obs) && !reset_count)
         return fail(HG_E_INVALID, "reset_index/final_obs need reset_count");
+    if (reset_count_next && (!reset_count || reset_count_next == reset_count))
+        return fail(HG_E_INVALID, "reset_count_next needs reset_count and must be another buffer");
     hipStream_t s = (hipStream_t)stream;
-    if (reset_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
+    bool zero_count = reset_count != nullptr;
+    if (reset_count_next) {
+        // chained: the previous step zeroed reset_count -- unless this launch is being captured into a
+        // graph (replays restart the rotation) or the previous one was (its zeroing may never run)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        HIP_TRY(hipStreamIsCapturing(s, &cs));
+        const bool capturing = cs != hipStreamCaptureStatusNone;
+        zero_count = capturing || e->chain_after_capture;
+        e->chain_after_capture = capturing;
+    }
+    if (zero_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
     const bool retrim = e->Pf.reset_retrim != 0 && e->Pf.autoreset != 0;   // auto-resets re-trimmed after the step
     if (retrim) HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
     StepArgs a;
@@ -1270,6 +1285,7 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
     a.info = info;
     a.eta = eta;
     a.reset_count = reset_count;
+    a.reset_count_next = reset_count_next;
     a.reset_index = reset_index;
     a.final_obs = final_obs;
     a.retrim_wind = e->retrim_wind;
@@ -1330,6 +1346,20 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
 #undef HG_LAUNCH_STEP
     HIP_TRY(hipGetLastError());
     return HG_OK;
+}
+
+int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count, int32_t* reset_index,
+                float* final_obs, void* stream) {
+    return step_impl(e, actions, obs, reward, terminated, truncated, info, eta, reset_count, reset_index, final_obs,
+                     nullptr, stream);
+}
+
+int32_t hg_step_chained(hg_env* e, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                        uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count,
+                        int32_t* reset_index, float* final_obs, int32_t* reset_count_next, void* stream) {
+    return step_impl(e, actions, obs, reward, terminated, truncated, info, eta, reset_count, reset_index, final_obs,
+                     reset_count_next, stream);
 }
 
 int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, float* reward, uint8_t* terminated,

@@ -95,6 +95,7 @@ _SIGS = {
     "hg_get_template": (ctypes.c_int32, [_P, ctypes.POINTER(hg_trim_result)]),
     "hg_reset": (ctypes.c_int32, [_P, _P, _P, _P]),
     "hg_step": (ctypes.c_int32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "hg_step_chained": (ctypes.c_int32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hg_get_state": (ctypes.c_int32, [_P, _P, _P, _P]),
     "hg_set_state": (ctypes.c_int32, [_P, _P, _P, _P]),
     "hg_random_actions": (ctypes.c_int32, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,

@@ -168,9 +168,14 @@ class HeliVecEnv(*_VEC_BASES):
         # info bits and reset info alternate between two buffer sets from step to step, so that the
         # lazily evaluated info of step() stays valid until the step after next (no copies, no sync)
         self._sets = [dict(info=torch.zeros((N,), dtype=u8, device=dev),
-                           count=torch.zeros((1,), dtype=i32, device=dev),
                            index=torch.empty((N,), dtype=i32, device=dev),
                            final=torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)) for _ in range(2)]
+        # reset counts rotate over three buffers: step k counts into ring[k % 3], which step k-1
+        # zeroed from inside its kernel (hg_step_chained: no separate zeroing launch), and zeroes
+        # ring[(k + 1) % 3]; step k's count is so readable until the step after next
+        self._count_ring = torch.zeros((3,), dtype=i32, device=dev)
+        self._ring_views = [self._count_ring[j:j + 1] for j in range(3)]
+        self._p_ring = [v.data_ptr() for v in self._ring_views]
         # the per-step host path passes plain addresses (no per-call tensor -> pointer conversions)
         # and reads the current stream through torch's raw-stream accessor
         self._dev_index = dev.index if dev.index is not None else torch.cuda.current_device()
@@ -180,7 +185,8 @@ class HeliVecEnv(*_VEC_BASES):
         self._term_b, self._trunc_b = self.terminated_u8.view(torch.bool), self.truncated_u8.view(torch.bool)
         self._act_shape = (N, _abi.HG_N_ACT)
         for b in self._sets:
-            b["p"] = tuple(b[k].data_ptr() for k in ("info", "count", "index", "final"))
+            b["count"] = self._ring_views[0]
+            b["p"] = tuple(b[k].data_ptr() for k in ("info", "index", "final"))
             b["thunks"] = self._info_thunks(b)
         self._gen = 0
         self._use_set(0)
@@ -199,6 +205,7 @@ class HeliVecEnv(*_VEC_BASES):
     # ------------------------------------------------------------------ plumbing
     def _use_set(self, g):
         b = self._sets[g & 1]
+        b["count"] = self._ring_views[g % 3]
         self.info_u8, self.reset_count, self.reset_index, self.final_obs = b["info"], b["count"], b["index"], b["final"]
         return b
 
@@ -209,7 +216,7 @@ class HeliVecEnv(*_VEC_BASES):
 
     def _info_thunks(self, b):
         """The lazy info fields of a step that used buffer set b: key -> f(info)."""
-        bits, cnt, index, final = b["info"], b["count"], b["index"], b["final"]
+        bits, index, final = b["info"], b["index"], b["final"]
         th = {"failed": lambda i: (bits & _abi.HG_INFO_FAILED) != 0,
               "successed": lambda i: (bits & _abi.HG_INFO_SUCCESSED) != 0,
               "time_up": lambda i: (bits & _abi.HG_INFO_TIME_UP) != 0,
@@ -218,7 +225,7 @@ class HeliVecEnv(*_VEC_BASES):
             def resets(i):   # (sorted env ids, their terminal observations); one host read per step
                 r = getattr(i, "_resets", None)
                 if r is None:
-                    k = int(cnt.item())
+                    k = int(b["count"].item())   # this set's step's ring slot
                     idx = index[:k].long()
                     order = self.torch.argsort(idx)
                     r = i._resets = (idx[order], final[:k][order])
@@ -287,9 +294,14 @@ class HeliVecEnv(*_VEC_BASES):
         b = self._use_set(self._gen)
         p = b["p"]
         rs = with_reset_info and self.autoreset and self.autoreset_mode == "same_step"
-        rc = self.lib.hg_step(self._h, a.data_ptr(), p_obs, self._p_rew, self._p_term, self._p_trunc, p[0],
-                              None if e is None else e.data_ptr(), p[1] if rs else None, p[2] if rs else None,
-                              p[3] if rs else None, self._stream())
+        g = self._gen
+        if rs:
+            rc = self.lib.hg_step_chained(self._h, a.data_ptr(), p_obs, self._p_rew, self._p_term, self._p_trunc,
+                                          p[0], None if e is None else e.data_ptr(), self._p_ring[g % 3], p[1], p[2],
+                                          self._p_ring[(g + 1) % 3], self._stream())
+        else:
+            rc = self.lib.hg_step(self._h, a.data_ptr(), p_obs, self._p_rew, self._p_term, self._p_trunc, p[0],
+                                  None if e is None else e.data_ptr(), None, None, None, self._stream())
         if rc:
             self._check(rc)
         return b

@@ -220,6 +220,17 @@ int32_t hg_step(hg_env* env, const float* actions_dev, float* obs_dev, float* re
                 const float* eta_dev, int32_t* reset_count_dev, int32_t* reset_index_dev,
                 float* final_obs_dev, void* stream);
 
+/* hg_step without the separate zeroing launch of the reset count: `reset_count_dev` must already be
+ * 0 (the previous chained step zeroed it), and this launch zeroes `reset_count_next_dev` (another
+ * buffer, for a later step) from inside the step kernel.  A caller rotating three count buffers
+ * (step k: count[k % 3], next count[(k + 1) % 3]) keeps each step's count readable until the step
+ * after next.  While `stream` is being captured into a graph, reset_count_dev is still zeroed by a
+ * memset node (a replayed graph restarts its buffer rotation).  Same results as hg_step. */
+int32_t hg_step_chained(hg_env* env, const float* actions_dev, float* obs_dev, float* reward_dev,
+                        uint8_t* terminated_dev, uint8_t* truncated_dev, uint8_t* info_dev,
+                        const float* eta_dev, int32_t* reset_count_dev, int32_t* reset_index_dev,
+                        float* final_obs_dev, int32_t* reset_count_next_dev, void* stream);
+
 /* Open-loop rollout: `nsteps` consecutive hg_step calls in one launch, each env's state kept in
  * registers between steps (state is read and written once).  Results are identical to nsteps
  * hg_step calls with the same inputs (same auto-reset, noise keys, flags).  Inputs / outputs are

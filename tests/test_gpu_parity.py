@@ -467,9 +467,10 @@ def test_ragged_batch_sizes(torch, n):
 @pytest.mark.parametrize("n", [1, 200, 4161])
 def test_reset_count_across_consecutive_launches(torch, n):
     """The reset compaction's count and the re-trim queue start from zero in every launch: over
-    consecutive eager and graph-replayed steps with resets in every step (staggered TimeLimit),
-    each step's count and index set equal its done flags; with auto-reset off a passed count
-    reads 0."""
+    consecutive eager (hg_step_chained: each step zeroes the next one's count) and graph-replayed
+    steps with resets in every step (staggered TimeLimit), and eager steps after a capture that is
+    never replayed, each step's count and index set equal its done flags; with auto-reset off a
+    passed count reads 0."""
     import ctypes
     from heligym_amd.vector import _ptr
     for mode in ("template", "retrim"):
@@ -497,6 +498,14 @@ def test_reset_count_across_consecutive_launches(torch, n):
             k = int(cnt_t.item())
             assert k == done.sum(), mode
             np.testing.assert_array_equal(np.sort(idx_t[:k].cpu().numpy()), np.nonzero(done)[0])
+        g2 = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g2):
+            env.step_async(act)   # captured and never replayed: its zeroing of the next count never runs
+        for _ in range(5):        # eager (hg_step_chained) again, after replays and after a dead capture
+            obs, rew, term, trunc, info = env.step(act)
+            done = (term | trunc).cpu().numpy()
+            assert int(env.reset_count.item()) == done.sum(), mode
+            np.testing.assert_array_equal(info["reset_index"].cpu().numpy(), np.nonzero(done)[0])
         env.close()
     env = make_env(torch, n, "hover", 0.01, autoreset=False)
     env.reset()
