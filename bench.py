@@ -461,8 +461,8 @@ def main():
         total_envs = N * world
 
         if not args.no_secondary and not args.dry_run:
-            # the same step with the user-facing reset info (same-step auto-reset: reset indices and
-            # terminal observations compacted in-kernel, one memset per step)
+            # the same step with the compacted reset info (same-step auto-reset: reset indices and
+            # terminal observations compacted in-kernel; captured, so a memset node zeroes the count)
             if args.reset_mode == "template":
                 def one_step_ri(k):
                     env.step_async(bank[k % B], with_reset_info=True)
@@ -471,8 +471,9 @@ def main():
                 del _k2
                 secondary["step_with_reset_info"] = {
                     "value": total_envs * K / s_ri, "unit": "env-steps/s", "ms_per_step": s_ri / K * 1e3,
-                    "note": "step_async(with_reset_info=True): reset_index + final_obs compaction, hipGraph"}
-                # HeliVecEnv.step(): host-synchronising API (reads the reset count every step), eager
+                    "note": "step_async(with_reset_info=True): reset_index + final_obs compaction "
+                            "(hg_step_chained; a memset node per captured step), hipGraph"}
+                # HeliVecEnv.step() as an RL loop calls it: eager, lazy info
                 Ke = min(K, 200)
 
                 def eager_api():
@@ -482,9 +483,10 @@ def main():
                 s_api, _, _ = timer.run(eager_api, 1)
                 secondary["step_api_eager"] = {
                     "value": total_envs * Ke / s_api, "unit": "env-steps/s", "ms_per_step": s_api / Ke * 1e3,
-                    "steps": Ke, "note": "HeliVecEnv.step() as an RL loop calls it: eager launch; its info dict "
-                                         "is lazy (fields not read here; the reset info costs a host read "
-                                         "of the reset count when read)"}
+                    "steps": Ke, "note": "HeliVecEnv.step() as an RL loop calls it: eager launch of the plain "
+                                         "kernel (hg_step_rows: reset envs flagged in the info bytes, their "
+                                         "terminal observations at their own rows); its info dict is lazy "
+                                         "(fields not read here; the reset info costs one nonzero when read)"}
             if env.specialized and not args.generic_kernel:
                 # the generic kernel (model constants loaded, any airframe); bitwise-identical results
                 env.set_specialized(False)

@@ -98,6 +98,7 @@ struct StepArgs {
     const float* eta;
     int32_t* reset_count;
     int32_t* reset_count_next;   // FEAT: zeroed by this launch for a later step (hg_step_chained), or NULL
+    float* final_obs_rows;       // [N,17] terminal observations of this step's auto-resets at their rows (hg_step_rows), or NULL
     int32_t* reset_index;
     float* final_obs;
     float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
@@ -444,17 +445,27 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     const bool done = term || trunc;
     succ += success_step ? 1 : 0;
 
+    // auto-reset (same step, or the step after the end)
+    const bool do_reset = P.autoreset && active && ((FEAT && P.autoreset_next) ? pending : done);
     if (active) {
         st_lane<NT>(a.reward + so + blk0, (uint32_t)tid, pending ? 0.f : rew);
         st_lane<NT>(a.terminated + so + blk0, (uint32_t)tid, (uint8_t)term);
         st_lane<NT>(a.truncated + so + blk0, (uint32_t)tid, (uint8_t)trunc);
         if (a.info)
             st_lane<NT>(a.info + so + blk0, (uint32_t)tid, pending ? (uint8_t)0 : (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
-                                  (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0)));
+                                  (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0) |
+                                  (do_reset ? HG_INFO_RESET : 0)));
+    }
+    // uncompacted reset info (hg_step_rows): the terminal observation at the env's own row, in a
+    // wave-uniform branch taken only by waves with a reset
+    if (!MULTI && a.final_obs_rows && __ballot(do_reset)) {
+        if (do_reset) {
+#pragma unroll
+            for (int c = 0; c < 17; ++c) a.final_obs_rows[i * 17 + c] = obs[c];
+        }
     }
 
-    // auto-reset (same step, or the step after the end) with a wave-ballot compaction
-    const bool do_reset = P.autoreset && active && ((FEAT && P.autoreset_next) ? pending : done);
+    // compacted reset info with a wave-ballot compaction
     if (FEAT && P.autoreset && a.reset_count) {
         const unsigned long long mask = __ballot(do_reset);
         if (mask) {
@@ -904,7 +915,8 @@ struct hg_env {
     bool baked = false;                     // step with the constant-specialised kernel (baked.h)
     bool baked_allowed = true;              // ... unless switched off (hg_set_specialized)
     hg::TrimSetup* setup_batch = nullptr;   // hg_trim_conds_batch scratch
-    bool chain_after_capture = true;        // hg_step_chained: re-zero the count (first call, after a capture)
+    bool chain_expect = false;              // the last step launch was a chained one, not captured: it zeroed
+                                            // the count the next hg_step_chained call counts into
     int64_t setup_batch_cap = 0;
 };
 
@@ -1248,7 +1260,8 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
 
 static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* reward, uint8_t* terminated,
                          uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count,
-                         int32_t* reset_index, float* final_obs, int32_t* reset_count_next, void* stream) {
+                         int32_t* reset_index, float* final_obs, int32_t* reset_count_next, float* final_obs_rows,
+                         void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
@@ -1264,12 +1277,15 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     bool zero_count = reset_count != nullptr;
     if (reset_count_next) {
         // chained: the previous step zeroed reset_count -- unless this launch is being captured into a
-        // graph (replays restart the rotation) or the previous one was (its zeroing may never run)
+        // graph (replays restart the rotation) or the previous step launch was not an executed
+        // chained one (another entry point, or a capture whose zeroing may never run)
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         HIP_TRY(hipStreamIsCapturing(s, &cs));
         const bool capturing = cs != hipStreamCaptureStatusNone;
-        zero_count = capturing || e->chain_after_capture;
-        e->chain_after_capture = capturing;
+        zero_count = capturing || !e->chain_expect;
+        e->chain_expect = !capturing;
+    } else {
+        e->chain_expect = false;
     }
     if (zero_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
     const bool retrim = e->Pf.reset_retrim != 0 && e->Pf.autoreset != 0;   // auto-resets re-trimmed after the step
@@ -1286,6 +1302,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.eta = eta;
     a.reset_count = reset_count;
     a.reset_count_next = reset_count_next;
+    a.final_obs_rows = final_obs_rows;
     a.reset_index = reset_index;
     a.final_obs = final_obs;
     a.retrim_wind = e->retrim_wind;
@@ -1352,14 +1369,21 @@ int32_t hg_step(hg_env* e, const float* actions, float* obs, float* reward, uint
                 uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count, int32_t* reset_index,
                 float* final_obs, void* stream) {
     return step_impl(e, actions, obs, reward, terminated, truncated, info, eta, reset_count, reset_index, final_obs,
-                     nullptr, stream);
+                     nullptr, nullptr, stream);
 }
 
 int32_t hg_step_chained(hg_env* e, const float* actions, float* obs, float* reward, uint8_t* terminated,
                         uint8_t* truncated, uint8_t* info, const float* eta, int32_t* reset_count,
                         int32_t* reset_index, float* final_obs, int32_t* reset_count_next, void* stream) {
     return step_impl(e, actions, obs, reward, terminated, truncated, info, eta, reset_count, reset_index, final_obs,
-                     reset_count_next, stream);
+                     reset_count_next, nullptr, stream);
+}
+
+int32_t hg_step_rows(hg_env* e, const float* actions, float* obs, float* reward, uint8_t* terminated,
+                     uint8_t* truncated, uint8_t* info, const float* eta, float* final_obs_rows, void* stream) {
+    if (final_obs_rows && !info) return fail(HG_E_INVALID, "hg_step_rows: final_obs_rows needs info (HG_INFO_RESET)");
+    return step_impl(e, actions, obs, reward, terminated, truncated, info, eta, nullptr, nullptr, nullptr, nullptr,
+                     final_obs_rows, stream);
 }
 
 int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, float* reward, uint8_t* terminated,
@@ -1374,6 +1398,7 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
         return fail(HG_E_INVALID, "actions and obs must be 16-byte aligned");
     if (e->Pf.reset_retrim)
         return fail(HG_E_INVALID, "hg_rollout does not support reset_mode RETRIM (re-trims run between steps)");
+    e->chain_expect = false;
     StepArgs a;
     memset(&a, 0, sizeof(a));
     a.state = e->state;

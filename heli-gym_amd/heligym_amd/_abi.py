@@ -20,7 +20,7 @@ HG_COUNTER_COLS = 3
 
 HG_OK = 0
 HG_TASK_HELI, HG_TASK_HOVER, HG_TASK_FORWARD_FLIGHT = 0, 1, 2
-HG_INFO_FAILED, HG_INFO_SUCCESSED, HG_INFO_TIME_UP, HG_INFO_SUCCESS_STEP = 1, 2, 4, 8
+HG_INFO_FAILED, HG_INFO_SUCCESSED, HG_INFO_TIME_UP, HG_INFO_SUCCESS_STEP, HG_INFO_RESET = 1, 2, 4, 8, 16
 HG_RESET_TEMPLATE, HG_RESET_RETRIM = 0, 1
 RESET_MODES = {"template": HG_RESET_TEMPLATE, "retrim": HG_RESET_RETRIM}
 HG_AUTORESET_SAME_STEP, HG_AUTORESET_NEXT_STEP = 0, 1
@@ -96,6 +96,7 @@ _SIGS = {
     "hg_reset": (ctypes.c_int32, [_P, _P, _P, _P]),
     "hg_step": (ctypes.c_int32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hg_step_chained": (ctypes.c_int32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "hg_step_rows": (ctypes.c_int32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "hg_get_state": (ctypes.c_int32, [_P, _P, _P, _P]),
     "hg_set_state": (ctypes.c_int32, [_P, _P, _P, _P]),
     "hg_random_actions": (ctypes.c_int32, [_P, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,

@@ -188,6 +188,7 @@ class HeliVecEnv(*_VEC_BASES):
             b["count"] = self._ring_views[0]
             b["p"] = tuple(b[k].data_ptr() for k in ("info", "index", "final"))
             b["thunks"] = self._info_thunks(b)
+            b["thunks_rows"] = self._info_thunks(b, rows=True)
         self._gen = 0
         self._use_set(0)
         # gymnasium.vector's convention: one env's spaces (helicopter.py:56-57) and the batched ones
@@ -214,14 +215,25 @@ class HeliVecEnv(*_VEC_BASES):
             return ctypes.c_void_p(self._raw_stream(self._dev_index))
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
-    def _info_thunks(self, b):
-        """The lazy info fields of a step that used buffer set b: key -> f(info)."""
+    def _info_thunks(self, b, rows=False):
+        """The lazy info fields of a step that used buffer set b: key -> f(info).  rows: the step
+        went through hg_step_rows (reset envs flagged by HG_INFO_RESET, terminal observations at
+        their own rows of b["final"]), else its reset info is the compacted one."""
         bits, index, final = b["info"], b["index"], b["final"]
         th = {"failed": lambda i: (bits & _abi.HG_INFO_FAILED) != 0,
               "successed": lambda i: (bits & _abi.HG_INFO_SUCCESSED) != 0,
               "time_up": lambda i: (bits & _abi.HG_INFO_TIME_UP) != 0,
               "success_step": lambda i: (bits & _abi.HG_INFO_SUCCESS_STEP) != 0}
-        if self.autoreset and self.autoreset_mode == "same_step":
+        if self.autoreset and self.autoreset_mode == "same_step" and rows:
+            def resets(i):   # (sorted env ids, their terminal observations); one nonzero per step
+                r = getattr(i, "_resets", None)
+                if r is None:
+                    idx = self.torch.nonzero(bits & _abi.HG_INFO_RESET).flatten()
+                    r = i._resets = (idx, final.index_select(0, idx))
+                return r
+            th["reset_index"] = lambda i: resets(i)[0]
+            th["final_obs"] = lambda i: resets(i)[1]
+        elif self.autoreset and self.autoreset_mode == "same_step":
             def resets(i):   # (sorted env ids, their terminal observations); one host read per step
                 r = getattr(i, "_resets", None)
                 if r is None:
@@ -271,8 +283,9 @@ class HeliVecEnv(*_VEC_BASES):
         buffering, e.g. while a previous step's observations are being gathered)."""
         self._launch(actions, eta, with_reset_info, obs_out)
 
-    def _launch(self, actions, eta, with_reset_info, obs_out):
-        """step_async's launch; returns the buffer set the step's info went to."""
+    def _launch(self, actions, eta, with_reset_info, obs_out, rows=False):
+        """step_async's launch; returns the buffer set the step's info went to.  rows: the reset
+        info uncompacted (hg_step_rows, step()'s path), else compacted (hg_step_chained)."""
         a = actions
         if a.dtype != self.torch.float32 or not a.is_contiguous() or a.device != self.device:
             a = a.to(device=self.device, dtype=self.torch.float32).contiguous()
@@ -295,7 +308,10 @@ class HeliVecEnv(*_VEC_BASES):
         p = b["p"]
         rs = with_reset_info and self.autoreset and self.autoreset_mode == "same_step"
         g = self._gen
-        if rs:
+        if rs and rows:
+            rc = self.lib.hg_step_rows(self._h, a.data_ptr(), p_obs, self._p_rew, self._p_term, self._p_trunc, p[0],
+                                       None if e is None else e.data_ptr(), p[2], self._stream())
+        elif rs:
             rc = self.lib.hg_step_chained(self._h, a.data_ptr(), p_obs, self._p_rew, self._p_term, self._p_trunc,
                                           p[0], None if e is None else e.data_ptr(), self._p_ring[g % 3], p[1], p[2],
                                           self._p_ring[(g + 1) % 3], self._stream())
@@ -310,10 +326,12 @@ class HeliVecEnv(*_VEC_BASES):
         """Heli.step (helicopter.py:192-206) for all envs: (obs, reward, terminated, truncated, info).
         Returned tensors are the env's buffers, overwritten by the next step.  `info` is evaluated
         lazily: a field costs its device ops (and, for the same-step reset info, a read of the reset
-        count) only when it is read, which must happen before the step after next."""
-        b = self._launch(actions, eta, True, None)
+        count) only when it is read, which must happen before the step after next.  The reset info
+        comes uncompacted (hg_step_rows: the reset envs' info bytes carry HG_INFO_RESET and their
+        terminal observations sit at their own rows), so the step is the plain kernel launch."""
+        b = self._launch(actions, eta, True, None, rows=True)
         gen = self._gen
-        info = LazyInfo(b["thunks"], lambda: self._gen - gen < 2)
+        info = LazyInfo(b["thunks_rows"], lambda: self._gen - gen < 2)
         return self.obs, self.reward, self._term_b, self._trunc_b, info
 
     # ------------------------------------------------------------------ setters (helicopter.py:89-111)

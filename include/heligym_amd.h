@@ -71,7 +71,8 @@ enum { HG_RESET_TEMPLATE = 0, HG_RESET_RETRIM = 1 };
 enum { HG_AUTORESET_SAME_STEP = 0, HG_AUTORESET_NEXT_STEP = 1 };
 
 /* info bit-field written per env by hg_step (helicopter.py:219-224). */
-enum { HG_INFO_FAILED = 1, HG_INFO_SUCCESSED = 2, HG_INFO_TIME_UP = 4, HG_INFO_SUCCESS_STEP = 8 };
+enum { HG_INFO_FAILED = 1, HG_INFO_SUCCESSED = 2, HG_INFO_TIME_UP = 4, HG_INFO_SUCCESS_STEP = 8,
+       HG_INFO_RESET = 16 /* auto-reset at the end of this step (same-step auto-reset) */ };
 
 /* Raw airframe + environment parameters: the fields of heligym/envs/helis/aw109.yaml:2-101. */
 typedef struct hg_airframe {
@@ -224,12 +225,23 @@ int32_t hg_step(hg_env* env, const float* actions_dev, float* obs_dev, float* re
  * 0 (the previous chained step zeroed it), and this launch zeroes `reset_count_next_dev` (another
  * buffer, for a later step) from inside the step kernel.  A caller rotating three count buffers
  * (step k: count[k % 3], next count[(k + 1) % 3]) keeps each step's count readable until the step
- * after next.  While `stream` is being captured into a graph, reset_count_dev is still zeroed by a
- * memset node (a replayed graph restarts its buffer rotation).  Same results as hg_step. */
+ * after next.  reset_count_dev is still zeroed by a memset launch when the handle's previous step
+ * launch was not an executed hg_step_chained call (the first call, after hg_step / hg_step_rows /
+ * hg_rollout) and while `stream` is being captured into a graph (a replayed graph restarts its
+ * buffer rotation).  Same results as hg_step. */
 int32_t hg_step_chained(hg_env* env, const float* actions_dev, float* obs_dev, float* reward_dev,
                         uint8_t* terminated_dev, uint8_t* truncated_dev, uint8_t* info_dev,
                         const float* eta_dev, int32_t* reset_count_dev, int32_t* reset_index_dev,
                         float* final_obs_dev, int32_t* reset_count_next_dev, void* stream);
+
+/* hg_step with the same-step reset info left uncompacted: the terminal observation of every env
+ * auto-reset in this step goes to its own row of `final_obs_rows_dev` [N,17] (other rows are left
+ * untouched) and its info byte carries HG_INFO_RESET, so the reset envs are the rows whose info has
+ * that bit.  No count, no atomics, no zeroing launch: the step runs the same kernel as a plain
+ * hg_step (the specialised one for the default airframe).  info_dev is required. */
+int32_t hg_step_rows(hg_env* env, const float* actions_dev, float* obs_dev, float* reward_dev,
+                     uint8_t* terminated_dev, uint8_t* truncated_dev, uint8_t* info_dev,
+                     const float* eta_dev, float* final_obs_rows_dev, void* stream);
 
 /* Open-loop rollout: `nsteps` consecutive hg_step calls in one launch, each env's state kept in
  * registers between steps (state is read and written once).  Results are identical to nsteps

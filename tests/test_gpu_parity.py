@@ -480,11 +480,17 @@ def test_reset_count_across_consecutive_launches(torch, n):
         ctr[:, 0] = torch.arange(n, device=env.device, dtype=torch.int32) % 3
         env.set_state(st, ctr)
         act = torch.zeros((n, 4), device=env.device)
-        for _ in range(7):
-            obs, rew, term, trunc, info = env.step(act)
-            done = (term | trunc).cpu().numpy()
-            assert int(env.reset_count.item()) == done.sum()
-            np.testing.assert_array_equal(info["reset_index"].cpu().numpy(), np.nonzero(done)[0])
+        def eager_checks(steps):   # step_async: the compacted reset info (hg_step_chained)
+            for _ in range(steps):
+                env.step_async(act)
+                done = (env.terminated_u8 | env.truncated_u8).cpu().numpy()
+                k = int(env.reset_count.item())
+                assert k == done.sum(), mode
+                np.testing.assert_array_equal(np.sort(env.reset_index[:k].cpu().numpy()), np.nonzero(done)[0])
+                obs, rew, term, trunc, info = env.step(act)   # and step()'s uncompacted one between
+                np.testing.assert_array_equal(info["reset_index"].cpu().numpy(),
+                                              np.nonzero((term | trunc).cpu().numpy())[0])
+        eager_checks(4)
         assert env.retrim_failures() == 0
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -501,11 +507,7 @@ def test_reset_count_across_consecutive_launches(torch, n):
         g2 = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g2):
             env.step_async(act)   # captured and never replayed: its zeroing of the next count never runs
-        for _ in range(5):        # eager (hg_step_chained) again, after replays and after a dead capture
-            obs, rew, term, trunc, info = env.step(act)
-            done = (term | trunc).cpu().numpy()
-            assert int(env.reset_count.item()) == done.sum(), mode
-            np.testing.assert_array_equal(info["reset_index"].cpu().numpy(), np.nonzero(done)[0])
+        eager_checks(3)   # eager again, after replays and after a dead capture
         env.close()
     env = make_env(torch, n, "hover", 0.01, autoreset=False)
     env.reset()
@@ -1184,6 +1186,36 @@ def test_reset_template_broadcast_partial_wave(torch, specialised, api):
     env.close()
 
 
+def test_step_rows_reset_info_equals_compacted(torch):
+    """step()'s uncompacted reset info (hg_step_rows: HG_INFO_RESET bits, terminal observations at
+    their own rows, the plain kernel) equals the compacted one (hg_step_chained: count, wave-ballot
+    index list, FEAT kernel) on a twin env, and every other output is bitwise the same."""
+    from heligym_amd import _abi
+    N = 2049
+    envs = [make_env(torch, N, "hover", 0.01, autoreset=True, seed=5) for _ in range(2)]
+    for e in envs:
+        e.reset()
+    act = torch.zeros((N, 4), dtype=torch.float32, device=envs[0].device)
+    act[: N // 3, 0] = -1.0
+    seen = 0
+    for k in range(400):
+        obs, rew, term, trunc, info = envs[0].step(act)
+        envs[1].step_async(act, with_reset_info=True)
+        cnt = int(envs[1].reset_count.item())
+        idx_c = envs[1].reset_index[:cnt].long()
+        order = torch.argsort(idx_c)
+        np.testing.assert_array_equal(info["reset_index"].cpu().numpy(), idx_c[order].cpu().numpy())
+        np.testing.assert_array_equal(info["final_obs"].cpu().numpy(), envs[1].final_obs[:cnt][order].cpu().numpy())
+        np.testing.assert_array_equal(((envs[0].info_u8 & _abi.HG_INFO_RESET) != 0).cpu().numpy(),
+                                      (term | trunc).cpu().numpy())
+        for x, y in ((obs, envs[1].obs), (rew, envs[1].reward), (envs[0].info_u8, envs[1].info_u8)):
+            np.testing.assert_array_equal(x.cpu().numpy(), y.cpu().numpy())
+        seen += cnt
+    assert seen > 0
+    for e in envs:
+        e.close()
+
+
 def test_lazy_info_matches_eager_and_expires(torch):
     """HeliVecEnv.step()'s info is evaluated lazily from double-buffered device buffers: a field
     read before the step after next equals the eager computation from that step's bits and reset
@@ -1198,8 +1230,8 @@ def test_lazy_info_matches_eager_and_expires(torch):
     for k in range(700):
         obs, rew, term, trunc, info = env.step(act)
         bits = env.info_u8.clone()
-        cnt = int(env.reset_count.item())
-        ref_idx = np.sort(env.reset_index[:cnt].cpu().numpy())
+        ref_idx = np.nonzero((term | trunc).cpu().numpy())[0]   # same-step auto-reset: every done env
+        cnt = len(ref_idx)
         if k % 2:   # read one step later (still valid)
             env.step_async(act)
         assert set(info) == {"failed", "successed", "time_up", "success_step", "reset_index", "final_obs"}
