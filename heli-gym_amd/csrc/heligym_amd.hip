@@ -103,9 +103,12 @@ struct StepArgs {
     float* final_obs;
     float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
     int32_t* retrim_list;    // ... compacted ids of the envs to re-trim
-    int32_t* retrim_count;   // ... their number (zeroed before the launch)
+    int32_t* retrim_count;   // ... their number: retrim_count[max(retrim_slot, 0)]
     const float* tmpl_env;   // per-env reset templates [N][39] (Params::env_templates), else unused
     int32_t nsteps;          // MULTI: steps per launch (inputs / outputs stacked [nsteps][N])
+    int32_t retrim_slot;     // -1, or the slot of retrim_count's ring of three this step counts into (it
+                             // zeroes the next one); in the padding before n: the kernel arguments stay
+                             // within 192 bytes, three scalar-cache lines (a fourth cost 0.23 us per step)
     int64_t n;
     uint64_t seed;
     int64_t env_offset;
@@ -344,7 +347,10 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
 #pragma unroll
     for (int c = 0; c < 18; ++c)   // ... and the heli state streams in behind the noise and wind work
         if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lt);
-    if (FEAT && a.reset_count_next && blockIdx.x == 0 && tid == 0) *a.reset_count_next = 0;
+    if (FEAT && blockIdx.x == 0 && tid == 0) {   // counters of a later step (rings of three)
+        if (a.reset_count_next) *a.reset_count_next = 0;
+        if (a.retrim_slot >= 0 && a.retrim_count) a.retrim_count[a.retrim_slot == 2 ? 0 : a.retrim_slot + 1] = 0;
+    }
     const int nsteps = MULTI ? a.nsteps : 1;
     for (int sstep = 0; sstep < nsteps; ++sstep) {
     // MULTI: the constants are re-read (scalar cache) each step rather than kept live across the
@@ -488,7 +494,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
         if (mask) {
             const int leader = __ffsll((long long)mask) - 1;
             int base = 0;
-            if (lane == leader) base = atomicAdd(a.retrim_count, __popcll(mask));
+            if (lane == leader) base = atomicAdd(a.retrim_count + (a.retrim_slot > 0 ? a.retrim_slot : 0), __popcll(mask));
             base = __shfl(base, leader);
             if (do_reset) a.retrim_list[base + __popcll(mask & ((1ull << lane) - 1ull))] = (int32_t)i;
         }
@@ -889,6 +895,19 @@ int32_t check_config(const hg_config* c, int32_t rows, int32_t cols) {
 
 // ------------------------------------------------------------------------------ handle
 
+// Counter rings (hg_step_chained's reset count, the re-trim job count): a step counts into its slot
+// and its kernel zeroes the next step's.  A launch may skip zeroing its own slot only when the
+// previous step launch was a chained one of the same sequence: both eager, or both captured into the
+// same graph (a graph's first step keeps its memset, so every replay starts from a zeroed slot).
+constexpr uint64_t kChainBroken = ~0ull;
+static hipError_t chain_key(hipStream_t s, uint64_t* key) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    const hipError_t err = hipStreamGetCaptureInfo(s, &cs, &id);
+    *key = cs == hipStreamCaptureStatusNone ? 0ull : (id | (1ull << 63));
+    return err;
+}
+
 struct hg_env {
     hg_config cfg;
     int device = 0;                          // the HIP device the handle's memory lives on
@@ -909,14 +928,16 @@ struct hg_env {
     Params<double>* pd_dev = nullptr;       // fp64 model constants for the re-trim kernel
     float* retrim_wind = nullptr;           // reset_mode RETRIM work buffers
     int32_t* retrim_list = nullptr;
-    int32_t* retrim_count = nullptr;        // [0] jobs of the current step, [1] failures so far
+    int32_t* retrim_count = nullptr;        // [0] jobs of hg_reset's re-trim, [1] failures so far
+    int32_t* retrim_ring = nullptr;         // [3] jobs of a step's re-trim: step k counts into [k % 3] and
+    uint64_t retrim_gen = 0;                //     zeroes [(k + 1) % 3] from its kernel (no memset launch)
+    uint64_t retrim_chain = kChainBroken;   // chain key of the previous re-trim step (see chain_key)
     float* tmpl_env = nullptr;              // per-env reset templates [N][39] (hg_set_reset_templates)
     bool env_templates = false;
     bool baked = false;                     // step with the constant-specialised kernel (baked.h)
     bool baked_allowed = true;              // ... unless switched off (hg_set_specialized)
     hg::TrimSetup* setup_batch = nullptr;   // hg_trim_conds_batch scratch
-    bool chain_expect = false;              // the last step launch was a chained one, not captured: it zeroed
-                                            // the count the next hg_step_chained call counts into
+    uint64_t chain_expect = kChainBroken;   // chain key of the previous step launch if it was a chained one
     int64_t setup_batch_cap = 0;
 };
 
@@ -1121,6 +1142,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     auto cleanup = [&](hipError_t err, const char* what) {
         dfree(e->hmap); dfree(e->state); dfree(e->tmpl_dev); dfree(e->params_dev);
         dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_count);
+        dfree(e->retrim_ring);
         dfree(e->tmpl_env); dfree(e->setup_batch);
         delete e;
         return fail(HG_E_HIP, std::string(what) + ": " + hipGetErrorString(err));
@@ -1151,6 +1173,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
         return cleanup(err, "hipMemcpy params64");
     if ((err = hipMalloc(&e->retrim_count, 2 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim");
     if ((err = hipMemset(e->retrim_count, 0, 2 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim");
+    if ((err = hipMalloc(&e->retrim_ring, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim ring");
+    if ((err = hipMemset(e->retrim_ring, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim ring");
     if (cfg->reset_mode == HG_RESET_RETRIM) {
         if ((err = hipMalloc(&e->retrim_wind, sizeof(float) * 3 * num_envs)) != hipSuccess)
             return cleanup(err, "hipMalloc retrim wind");
@@ -1180,6 +1204,7 @@ void hg_destroy(hg_env* e) {
     dfree(e->retrim_wind);
     dfree(e->retrim_list);
     dfree(e->retrim_count);
+    dfree(e->retrim_ring);
     dfree(e->tmpl_env);
     dfree(e->setup_batch);
     delete e;
@@ -1275,21 +1300,25 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         return fail(HG_E_INVALID, "reset_count_next needs reset_count and must be another buffer");
     hipStream_t s = (hipStream_t)stream;
     bool zero_count = reset_count != nullptr;
-    if (reset_count_next) {
-        // chained: the previous step zeroed reset_count -- unless this launch is being captured into a
-        // graph (replays restart the rotation) or the previous step launch was not an executed
-        // chained one (another entry point, or a capture whose zeroing may never run)
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        HIP_TRY(hipStreamIsCapturing(s, &cs));
-        const bool capturing = cs != hipStreamCaptureStatusNone;
-        zero_count = capturing || !e->chain_expect;
-        e->chain_expect = !capturing;
+    uint64_t key = 0;
+    const bool retrim = e->Pf.reset_retrim != 0 && e->Pf.autoreset != 0;   // auto-resets re-trimmed after the step
+    if (reset_count_next || retrim) HIP_TRY(chain_key(s, &key));
+    if (reset_count_next) {   // chained: the previous step zeroed reset_count if it was of the same sequence
+        zero_count = e->chain_expect != key;
+        e->chain_expect = key;
     } else {
-        e->chain_expect = false;
+        e->chain_expect = kChainBroken;
     }
     if (zero_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
-    const bool retrim = e->Pf.reset_retrim != 0 && e->Pf.autoreset != 0;   // auto-resets re-trimmed after the step
-    if (retrim) HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
+    int32_t* rt_count = nullptr;
+    int32_t rt_slot = -1;
+    if (retrim) {   // the step's re-trim job count: a slot of the ring, zeroed by the previous step's kernel
+        rt_slot = (int32_t)(e->retrim_gen % 3);
+        rt_count = e->retrim_ring + rt_slot;
+        ++e->retrim_gen;
+        if (e->retrim_chain != key) HIP_TRY(hipMemsetAsync(rt_count, 0, sizeof(int32_t), s));
+        e->retrim_chain = key;
+    }
     StepArgs a;
     a.state = e->state;
     a.hmap = e->hmap;
@@ -1307,7 +1336,8 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.final_obs = final_obs;
     a.retrim_wind = e->retrim_wind;
     a.retrim_list = e->retrim_list;
-    a.retrim_count = e->retrim_count;
+    a.retrim_count = retrim ? e->retrim_ring : e->retrim_count;   // (unused unless auto-resets re-trim)
+    a.retrim_slot = rt_slot;
     a.tmpl_env = e->tmpl_env;
     a.nsteps = 1;
     a.n = e->n;
@@ -1351,7 +1381,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         memset(&r, 0, sizeof(r));
         r.P = e->pd_dev;
         r.T = e->setup_dev;
-        r.count = e->retrim_count;
+        r.count = rt_count;
         r.list = e->retrim_list;
         r.wind = e->retrim_wind;
         r.state = e->state;
@@ -1398,7 +1428,7 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
         return fail(HG_E_INVALID, "actions and obs must be 16-byte aligned");
     if (e->Pf.reset_retrim)
         return fail(HG_E_INVALID, "hg_rollout does not support reset_mode RETRIM (re-trims run between steps)");
-    e->chain_expect = false;
+    e->chain_expect = kChainBroken;
     StepArgs a;
     memset(&a, 0, sizeof(a));
     a.state = e->state;
@@ -1412,6 +1442,7 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     a.eta = eta;
     a.tmpl_env = e->tmpl_env;
     a.nsteps = nsteps;
+    a.retrim_slot = -1;
     a.n = e->n;
     a.seed = e->cfg.seed;
     a.env_offset = e->cfg.env_offset;

@@ -226,9 +226,9 @@ int32_t hg_step(hg_env* env, const float* actions_dev, float* obs_dev, float* re
  * buffer, for a later step) from inside the step kernel.  A caller rotating three count buffers
  * (step k: count[k % 3], next count[(k + 1) % 3]) keeps each step's count readable until the step
  * after next.  reset_count_dev is still zeroed by a memset launch when the handle's previous step
- * launch was not an executed hg_step_chained call (the first call, after hg_step / hg_step_rows /
- * hg_rollout) and while `stream` is being captured into a graph (a replayed graph restarts its
- * buffer rotation).  Same results as hg_step. */
+ * launch was not an hg_step_chained call of the same sequence -- the first call, after hg_step /
+ * hg_step_rows / hg_rollout, the first call captured into a graph (so that every replay starts
+ * from a zeroed count) and the first eager call after a capture.  Same results as hg_step. */
 int32_t hg_step_chained(hg_env* env, const float* actions_dev, float* obs_dev, float* reward_dev,
                         uint8_t* terminated_dev, uint8_t* truncated_dev, uint8_t* info_dev,
                         const float* eta_dev, int32_t* reset_count_dev, int32_t* reset_index_dev,
