@@ -86,8 +86,16 @@ __device__ __forceinline__ float u01(uint32_t x) {   // (0, 1)
 
 // ------------------------------------------------------------------------------ kernels
 
+// Kernel arguments.  Order matters: the first scalar load of the kernel (64 bytes after the two
+// pointer parameters) carries everything the state loads wait for -- the state base, n (a lane is
+// active), the noise key -- so no second scalar-load round trip sits in front of them; the
+// feature-only fields come last.  192 bytes in all, three scalar-cache lines (200 bytes, a fourth
+// line, cost 0.23 us per step).
 struct StepArgs {
     float* state;            // wave tiles (tix): state columns then counters
+    int64_t n;
+    uint64_t seed;
+    int64_t env_offset;
     const float2* hmap;
     const float* actions;
     float* obs;
@@ -96,22 +104,19 @@ struct StepArgs {
     uint8_t* truncated;
     uint8_t* info;
     const float* eta;
-    int32_t* reset_count;
-    int32_t* reset_count_next;   // FEAT: zeroed by this launch for a later step (hg_step_chained), or NULL
     float* final_obs_rows;       // [N,17] terminal observations of this step's auto-resets at their rows (hg_step_rows), or NULL
+    int32_t nsteps;          // MULTI: steps per launch (inputs / outputs stacked [nsteps][N])
+    int32_t retrim_slot;     // -1, or the slot of retrim_count's ring of three this step counts into (it
+                             // zeroes the next one)
+    // FEAT only
+    int32_t* reset_count;
+    int32_t* reset_count_next;   // zeroed by this launch for a later step (hg_step_chained), or NULL
     int32_t* reset_index;
     float* final_obs;
     float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
     int32_t* retrim_list;    // ... compacted ids of the envs to re-trim
     int32_t* retrim_count;   // ... their number: retrim_count[max(retrim_slot, 0)]
     const float* tmpl_env;   // per-env reset templates [N][39] (Params::env_templates), else unused
-    int32_t nsteps;          // MULTI: steps per launch (inputs / outputs stacked [nsteps][N])
-    int32_t retrim_slot;     // -1, or the slot of retrim_count's ring of three this step counts into (it
-                             // zeroes the next one); in the padding before n: the kernel arguments stay
-                             // within 192 bytes, three scalar-cache lines (a fourth cost 0.23 us per step)
-    int64_t n;
-    uint64_t seed;
-    int64_t env_offset;
 };
 
 // Model constants travel as a pointer to a device copy (scalar loads); by value they would take
