@@ -86,16 +86,13 @@ __device__ __forceinline__ float u01(uint32_t x) {   // (0, 1)
 
 // ------------------------------------------------------------------------------ kernels
 
-// Kernel arguments.  Order matters: the first scalar load of the kernel (64 bytes after the two
-// pointer parameters) carries everything the state loads wait for -- the state base, n (a lane is
-// active), the noise key -- so no second scalar-load round trip sits in front of them; the
-// feature-only fields come last.  192 bytes in all, three scalar-cache lines (200 bytes, a fourth
-// line, cost 0.23 us per step).
+// Kernel arguments.  What the state loads wait for -- the state base, n (a lane is active), the noise
+// key -- are the step kernel's first scalar parameters, preloaded into SGPRs at wave launch
+// (-amdgpu-kernarg-preload-count), so no scalar-load round trip sits in front of the state loads;
+// StepArgs follows, its feature-only fields last.  192 bytes in all, three scalar-cache lines (200
+// bytes, a fourth line on the critical path, cost 0.23 us per step).
+constexpr int kStepPreloadArgs = 6;   // state, n, seed, env_offset, Pa, Tp
 struct StepArgs {
-    float* state;            // wave tiles (tix): state columns then counters
-    int64_t n;
-    uint64_t seed;
-    int64_t env_offset;
     const float2* hmap;
     const float* actions;
     float* obs;
@@ -254,7 +251,8 @@ __device__ __forceinline__ void rk_update(float* hs, const float* k, const float
 // Turbulence noise of a step (wind_dynamics.py:49-52: eta = randn(3) / sqrt(dt)): injected by the
 // caller (ETA), or Box-Muller normals from Philox4x32-10 keyed by (global env id, step, episode).
 template <bool ETA>
-__device__ __forceinline__ void draw_eta(const StepArgs& a, const Params<float>& P, int64_t so, int64_t blk0,
+__device__ __forceinline__ void draw_eta(const StepArgs& a, uint64_t seed, int64_t env_offset, const Params<float>& P,
+                                         int64_t so, int64_t blk0,
                                          uint32_t lo, int32_t step, int32_t epi, float eta[3]) {
     if (ETA) {
         const float* eb = a.eta + 3 * (so + blk0);
@@ -262,9 +260,9 @@ __device__ __forceinline__ void draw_eta(const StepArgs& a, const Params<float>&
         eta[1] = ld_lane(eb + 1, 3 * lo);
         eta[2] = ld_lane(eb + 2, 3 * lo);
     } else {
-        const uint64_t gid = (uint64_t)(a.env_offset + blk0 + lo);
+        const uint64_t gid = (uint64_t)(env_offset + blk0 + lo);
         const U4 r = philox(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)epi},
-                            (uint32_t)a.seed, (uint32_t)(a.seed >> 32));
+                            (uint32_t)seed, (uint32_t)(seed >> 32));
         float sn, cs;
         const float r0 = sqrtf(-2.f * __logf(u01(r.x)));
         __sincosf(6.28318530717958648f * u01(r.y), &sn, &cs);
@@ -304,8 +302,9 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
 // instruction literals (baked.h), the runtime fields still read from the device copy.  All
 // compile-time, so the hot kernel has no data-independent branches to merge around.
 template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
-__global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(ParamArg Pa, const Template<float>* __restrict__ Tp,
-                                                      const StepArgs a) {
+__global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p,
+                                                      int64_t envoff_p, ParamArg Pa,
+                                                      const Template<float>* __restrict__ Tp, const StepArgs a) {
     __shared__ float s_obs[kStepBlock * HG_N_OBS];   // one 64-row slice per wave
     const Params<float>& P0 = *Pa;   // model constants: scalar loads from a device copy
     // BAKED: the default airframe's constants as instruction literals (baked.h); only the runtime
@@ -321,7 +320,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     const int64_t blk0 = tile * 64;   // this wave's first env
     const int tid = lane;
     const int64_t i = blk0 + tid;
-    const int64_t n = a.n;
+    const int64_t n = n_p;
     const bool active = i < n;
     // Addressing: this wave's state tile (64 envs x 30 columns, contiguous) from one uniform (SGPR)
     // base at its middle column, so every column is an immediate offset (+-3.8 KB, inside the 13-bit
@@ -331,7 +330,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     const uint32_t lo = (uint32_t)(active ? tid : 0);
     const uint32_t lt = (uint32_t)tid;
 #define COL(ptr, c) ((ptr) + ((c) - 15) * kTileEnvs)
-    float* st_b = a.state + (blk0 / kTileEnvs) * kTileWords + (blk0 % kTileEnvs) + 15 * kTileEnvs;
+    float* st_b = state_p + (blk0 / kTileEnvs) * kTileWords + (blk0 % kTileEnvs) + 15 * kTileEnvs;
     int32_t* ct_b = reinterpret_cast<int32_t*>(st_b);
 
 #if HG_TIMING
@@ -370,7 +369,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     TSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(epi), "v"(carry[3]), "v"(ws[4]));
     // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
     float eta[3];
-    draw_eta<ETA>(a, P, so, blk0, lo, step, epi, eta);
+    draw_eta<ETA>(a, seed_p, envoff_p, P, so, blk0, lo, step, epi, eta);
 
     // ground height under the committed position (F6), wind step (Heli.step :195-199)
     TSTAMP(2, "v"(eta[2]), "v"(eta[0]));
@@ -549,7 +548,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     store_obs_wave<NT, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, a.obs, so, blk0, n, lane);
     }   // steps
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
-    st_b = a.state + (blk0 / kTileEnvs) * kTileWords + (blk0 % kTileEnvs) + 15 * kTileEnvs;
+    st_b = state_p + (blk0 / kTileEnvs) * kTileWords + (blk0 % kTileEnvs) + 15 * kTileEnvs;
     asm volatile("" : "+s"(st_b));
     ct_b = reinterpret_cast<int32_t*>(st_b);
     if (active) {
@@ -1013,11 +1012,13 @@ static inline unsigned retrim_grid(int64_t jobs) {
 }
 
 #define PARAM_ARG(e) ((const Params<float>*)(e)->params_dev)
+// the step kernel's leading (preloaded) parameters
+#define STEP_KARGS(e) (e)->state, (int64_t)(e)->n, (uint64_t)(e)->cfg.seed, (int64_t)(e)->cfg.env_offset, PARAM_ARG(e), \
+                      (e)->tmpl_dev
 
 // The default airframe's constant-specialised step (baked.h), with or without the optional features.
 #define HG_LAUNCH_SPECIALISED(T, ETA_, NT_, FEAT_, MULTI_)                                                 \
-    hipLaunchKernelGGL((step_kernel<T, ETA_, NT_, FEAT_, MULTI_, true>), grid, block, 0, s, PARAM_ARG(e),  \
-                       e->tmpl_dev, a)
+    hipLaunchKernelGGL((step_kernel<T, ETA_, NT_, FEAT_, MULTI_, true>), grid, block, 0, s, STEP_KARGS(e), a)
 
 extern "C" {
 #if HG_TIMING
@@ -1325,7 +1326,6 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         e->retrim_chain = key;
     }
     StepArgs a;
-    a.state = e->state;
     a.hmap = e->hmap;
     a.actions = actions;
     a.obs = obs;
@@ -1345,9 +1345,6 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.retrim_slot = rt_slot;
     a.tmpl_env = e->tmpl_env;
     a.nsteps = 1;
-    a.n = e->n;
-    a.seed = e->cfg.seed;
-    a.env_offset = e->cfg.env_offset;
     const dim3 grid((unsigned)((e->n + kStepBlock - 1) / kStepBlock)), block(kStepBlock);
     const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next ||
                       e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
@@ -1362,11 +1359,11 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
                 else HG_LAUNCH_SPECIALISED(T, false, NT, false, false);                                          \
             }                                                                                                    \
         } else if (feat) {                                                                                       \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false, false>), grid, block, 0, s, STEP_KARGS(e), a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false, false>), grid, block, 0, s, STEP_KARGS(e), a);    \
         } else {                                                                                                 \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false, false>), grid, block, 0, s, STEP_KARGS(e), a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false, false>), grid, block, 0, s, STEP_KARGS(e), a);    \
         }                                                                                                        \
     } while (0)
 #define HG_LAUNCH_STEP(T)                                   \
@@ -1436,7 +1433,6 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     e->chain_expect = kChainBroken;
     StepArgs a;
     memset(&a, 0, sizeof(a));
-    a.state = e->state;
     a.hmap = e->hmap;
     a.actions = actions;
     a.obs = obs;
@@ -1448,9 +1444,6 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     a.tmpl_env = e->tmpl_env;
     a.nsteps = nsteps;
     a.retrim_slot = -1;
-    a.n = e->n;
-    a.seed = e->cfg.seed;
-    a.env_offset = e->cfg.env_offset;
     hipStream_t s = (hipStream_t)stream;
     const dim3 grid((unsigned)((e->n + kStepBlock - 1) / kStepBlock)), block(kStepBlock);
     const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
@@ -1465,11 +1458,11 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
                 else HG_LAUNCH_SPECIALISED(T, false, NT, false, true);                                           \
             }                                                                                                    \
         } else if (feat) {                                                                                       \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true, false>), grid, block, 0, s, STEP_KARGS(e), a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true, false>), grid, block, 0, s, STEP_KARGS(e), a);    \
         } else {                                                                                                 \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, false>), grid, block, 0, s, PARAM_ARG(e), e->tmpl_dev, a);    \
+            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, false>), grid, block, 0, s, STEP_KARGS(e), a); \
+            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, false>), grid, block, 0, s, STEP_KARGS(e), a);    \
         }                                                                                                        \
     } while (0)
 #define HG_LAUNCH_ROLL(T)                                   \
