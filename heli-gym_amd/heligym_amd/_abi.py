@@ -25,7 +25,7 @@ HG_RESET_TEMPLATE, HG_RESET_RETRIM = 0, 1
 RESET_MODES = {"template": HG_RESET_TEMPLATE, "retrim": HG_RESET_RETRIM}
 HG_AUTORESET_SAME_STEP, HG_AUTORESET_NEXT_STEP = 0, 1
 AUTORESET_MODES = {"same_step": HG_AUTORESET_SAME_STEP, "next_step": HG_AUTORESET_NEXT_STEP}
-HG_ABI_VERSION = 2
+HG_ABI_VERSION = 3
 
 AIRFRAME_FIELDS = (
     ["env_R", "env_T0", "env_LAPSE", "env_RO_SEA", "env_GRAV", "env_MAX_GR_ALT", "env_NS_MAX",

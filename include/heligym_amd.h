@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 2
+#define HG_ABI_VERSION 3
 
 #define HG_N_OBS 17        /* helicopter_dynamics.py:23-27 */
 #define HG_N_ACT 4         /* helicopter_dynamics.py:28 */
