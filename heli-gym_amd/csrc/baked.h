@@ -34,7 +34,17 @@
     X(wm[0]) X(wm[1]) X(wm[2]) X(wind_dir_cos) X(wind_dir_sin) X(w20) X(sigma_low) X(turb_level)    \
     X(tep_row[0]) X(tep_row[1]) X(tep_row[2]) X(tep_row[3]) X(tep_row[4]) X(tep_row[5])             \
     X(tep_row[6]) X(tep_row[7]) X(tep_row[8]) X(tep_row[9]) X(tep_row[10]) X(tep_row[11])           \
-    X(tep_row[12]) X(n_t) X(n_t2) X(inv_n_x) X(inv_n_v) X(inv_n_a) X(fail_zdot) X(fail_ang)
+    X(tep_row[12]) X(n_t) X(n_t2) X(inv_n_x) X(inv_n_v) X(inv_n_a) X(fail_zdot) X(fail_ang)        \
+    X(f_kc_irho) X(f_og_irho) X(f_mr_inflow_thr) X(f_tr_inflow_thr) X(f_mr_ct_k) X(f_mr_db_a)       \
+    X(f_mr_db_b) X(f_hXUU) X(f_hYVV) X(f_hZWW) X(f_zd) X(f_m2_R) X(f_rho_lz) X(f_gyro[0]) X(f_gyro[1])    \
+    X(f_gyro[2]) X(f_gyro[3]) X(f_gyro[4]) X(f_gyro[5])
+
+// The fields that stay runtime values in the baked kernel (dt, task, target, limits, flags): with
+// HG_BAKED_FIELDS they cover every field of Params<float> (checked below).
+#define HG_RUNTIME_FIELDS(X)                                                                        \
+    X(dt) X(half_dt) X(dt6) X(eta_norm) X(tgt_n[0]) X(tgt_n[1]) X(tgt_n[2]) X(vel_tgt_n)            \
+    X(dwn_tgt_n) X(task) X(time_up_steps) X(success_steps) X(autoreset) X(reset_retrim)            \
+    X(autoreset_next) X(max_episode_steps) X(env_templates) X(f_dpsi_mr) X(f_dpsi_tr)
 
 namespace hg {
 
@@ -48,11 +58,20 @@ constexpr Params<float> kBakedAW109 = __builtin_bit_cast(Params<float>, ParamWor
 #include "baked_aw109.inc"
 }});
 
-// Overwrite the baked fields of a (runtime) Params with the compiled-in literals.
-HD void bake(Params<float>& P) {
-#define HG_BAKE_ONE(f) P.f = kBakedAW109.f;
-    HG_BAKED_FIELDS(HG_BAKE_ONE)
-#undef HG_BAKE_ONE
+#define HG_FIELD_BYTES(f) +sizeof(((const Params<float>*)nullptr)->f)
+static_assert(0 HG_BAKED_FIELDS(HG_FIELD_BYTES) HG_RUNTIME_FIELDS(HG_FIELD_BYTES) == sizeof(Params<float>),
+              "every Params field must be listed as baked or runtime");
+#undef HG_FIELD_BYTES
+
+// The compiled-in constants with the runtime fields of R.  Built from the constant image (not by
+// overwriting a copy of R field by field), so the optimiser sees one constant object plus a few
+// scalar stores and keeps every field in a register or an instruction literal.
+HD Params<float> bake(const Params<float>& R) {
+    Params<float> P = kBakedAW109;
+#define HG_RT_ONE(f) P.f = R.f;
+    HG_RUNTIME_FIELDS(HG_RT_ONE)
+#undef HG_RT_ONE
+    return P;
 }
 
 // True when every baked field of P equals the compiled-in value bit for bit.

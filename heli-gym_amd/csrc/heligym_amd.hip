@@ -25,6 +25,7 @@
 #include "trim.h"
 #include "retrim.h"
 #include "baked.h"
+#include "stage_f32.h"
 
 using hg::Params;
 using hg::Template;
@@ -310,10 +311,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     // BAKED: the default airframe's constants as instruction literals (baked.h); only the runtime
     // fields (dt, target, limits, flags) are loaded
     Params<float> PB;
-    if constexpr (BAKED) {
-        PB = *Pa;
-        hg::bake(PB);
-    }
+    if constexpr (BAKED) PB = hg::bake(*Pa);
     const int lane = threadIdx.x & 63;
     const int wv = kStepBlock == 64 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
     const int64_t tile = (int64_t)blockIdx.x * (kStepBlock / 64) + wv;
@@ -380,21 +378,9 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
 
     TSTAMP(4, "v"(h_c.delta), "v"(h_c.hi));
     // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
-    const hg::Controls<float> u = hg::controls(P, act.x, act.y, act.z, act.w);
-    float k[18], acc[18], st[18], obs[17];
-    const hg::Attitude<float> att0 = hg::attitude(hs + 12);
-    float e0[3] = {hs[12], hs[13], hs[14]};
-    hg::dynamics<false>(P, hs, u, W, h_c, att0, k, obs);
-    TSTAMP(5, "v"(k[8]), "v"(k[11]));
-    rk_stage<true>(hs, k, acc, st, P.half_dt);
-    hg::dynamics<false>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
-    TSTAMP(6, "v"(k[8]), "v"(k[11]));
-    rk_stage<false>(hs, k, acc, st, P.half_dt);
-    hg::dynamics<false>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
-    TSTAMP(7, "v"(k[8]), "v"(k[11]));
-    rk_stage<false>(hs, k, acc, st, P.dt);
-    hg::dynamics<true>(P, st, u, W, h_c, hg::attitude_step(att0, e0, st + 12), k, obs);
-    rk_update(hs, k, acc, P.dt6);
+    const hg::StepCtx ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, W[0], W[1], W[2], h_c, hs[17]);
+    float k[18], obs[17];
+    hg::rk4_step_f32(P, ctx, hs, k, obs);
 #if HG_EARLY_POST
     // the terrain texels under the post-step position (the flags' ground height), requested now so
     // that their latency hides behind the wraps and the reward
@@ -485,8 +471,8 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
             base = __shfl(base, leader);
             if (do_reset) {
                 const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
-                if (a.reset_index) a.reset_index[slot] = (int32_t)i;
-                if (a.final_obs) {
+                if (a.reset_index && slot < n) a.reset_index[slot] = (int32_t)i;
+                if (a.final_obs && slot < n) {
 #pragma unroll
                     for (int c = 0; c < 17; ++c) a.final_obs[(int64_t)slot * 17 + c] = obs[c];
                 }
@@ -500,7 +486,8 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
             int base = 0;
             if (lane == leader) base = atomicAdd(a.retrim_count + (a.retrim_slot > 0 ? a.retrim_slot : 0), __popcll(mask));
             base = __shfl(base, leader);
-            if (do_reset) a.retrim_list[base + __popcll(mask & ((1ull << lane) - 1ull))] = (int32_t)i;
+            const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
+            if (do_reset && slot < n) a.retrim_list[slot] = (int32_t)i;
         }
     }
     if (FEAT && P.env_templates) {   // this env's own reset target (its own trim condition)
@@ -786,6 +773,33 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
     P.turb_level = (R)a.env_TURB_LVL;
     hg::tep_row_values(P.turb_level, P.tep_row);
     P.eta_norm = (R)(1.0 / sqrt(dt));
+    // folded constants of the packed fp32 step (stage_f32.h), formed in double
+    P.f_kc_irho = (R)(0.75 * mr_OM * a.mr_E / a.mr_R / gam_dro);
+    P.f_og_irho = (R)(mr_OM / gam_dro);
+    P.f_mr_inflow_thr = (R)(0.75 * M_PI / a.mr_R * (0.25 * mr_VT * a.mr_R * a.mr_A * a.mr_B * a.mr_C) /
+                            (2 * M_PI * a.mr_R * a.mr_R));
+    P.f_tr_inflow_thr = (R)(0.5 * 0.75 * M_PI / a.tr_R * (0.25 * tr_VT * a.tr_R * a.tr_A * a.tr_B * a.tr_C) /
+                            (2 * M_PI * a.tr_R * a.tr_R));
+    P.f_mr_ct_k = (R)((0.25 * mr_VT * a.mr_R * a.mr_A * a.mr_B * a.mr_C) / (M_PI * a.mr_R * a.mr_R * mr_VT * mr_VT));
+    P.f_mr_db_a = (R)(2.0 / mr_VT * 8.0 / mr_ASIG);
+    P.f_mr_db_b = (R)(0.5 * (2.0 / mr_VT) * (2.0 / mr_VT));
+    P.f_hXUU = (R)(0.5 * a.fus_XUU);
+    P.f_hYVV = (R)(0.5 * a.fus_YVV);
+    P.f_hZWW = (R)(0.5 * a.fus_ZWW);
+    P.f_zd = (R)(-0.5 * a.fus_ZWW * a.fus_COR);
+    P.f_m2_R = (R)(-2.0 / a.mr_R);
+    P.f_rho_lz = (R)((a.env_GRAV / (a.env_LAPSE * a.env_R) - 1.0) * a.env_LAPSE / a.env_T0);
+    {   // gyroscopic coefficients (stage_f32.h): g = M - pqr x I pqr, (p', q', r') = I^-1 g
+        const double J00 = Iz / det, J02 = -Ixz / det, J20 = -Ixz / det, J22 = Ix / det, J11 = 1.0 / Iy;
+        P.f_gyro[0] = (R)(-(J00 * Ixz + J02 * (Iy - Ix)));   // p' per pq
+        P.f_gyro[1] = (R)(-(J20 * Ixz + J22 * (Iy - Ix)));   // r' per pq
+        P.f_gyro[2] = (R)(-(J00 * (Iz - Iy) - J02 * Ixz));  // p' per qr
+        P.f_gyro[3] = (R)(-(J20 * (Iz - Iy) - J22 * Ixz));  // r' per qr
+        P.f_gyro[4] = (R)(-J11 * (Ix - Iz));                 // q' per pr
+        P.f_gyro[5] = (R)(-J11 * Ixz);                       // q' per r^2 - p^2
+    }
+    P.f_dpsi_mr = (R)(dt * mr_OM);
+    P.f_dpsi_tr = (R)(dt * tr_OM);
     // task (helicopter.py:63-68, helicopter_with_tasks.py:33, 87-88)
     const double n_t = sqrt(2 * a.mr_R / a.env_GRAV), n_x = 2 * a.mr_R, n_v = sqrt(2 * a.mr_R * a.env_GRAV);
     P.n_t = (R)n_t; P.n_t2 = (R)(n_t * n_t);
@@ -942,6 +956,8 @@ struct hg_env {
     bool baked_allowed = true;              // ... unless switched off (hg_set_specialized)
     hg::TrimSetup* setup_batch = nullptr;   // hg_trim_conds_batch scratch
     uint64_t chain_expect = kChainBroken;   // chain key of the previous step launch if it was a chained one
+    bool ever_captured = false;             // a step was captured into a graph: replays the host cannot see may
+                                            // leave any ring slot non-zero, so eager steps zero their own slot
     int64_t setup_batch_cap = 0;
 };
 
@@ -1309,8 +1325,14 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     uint64_t key = 0;
     const bool retrim = e->Pf.reset_retrim != 0 && e->Pf.autoreset != 0;   // auto-resets re-trimmed after the step
     if (reset_count_next || retrim) HIP_TRY(chain_key(s, &key));
+    if (key != 0) e->ever_captured = true;
+    // Once any step was captured, a replay of that graph (invisible here) may run between two eager
+    // launches and leave the slot the next eager step counts into non-zero: eager steps then always
+    // zero their own slot.  Inside one capture the graph's first step zeroes its slot (chain key of
+    // a new capture) and each captured kernel zeroes the next one's, so every replay starts clean.
+    const bool eager_after_capture = key == 0 && e->ever_captured;
     if (reset_count_next) {   // chained: the previous step zeroed reset_count if it was of the same sequence
-        zero_count = e->chain_expect != key;
+        zero_count = e->chain_expect != key || eager_after_capture;
         e->chain_expect = key;
     } else {
         e->chain_expect = kChainBroken;
@@ -1322,7 +1344,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         rt_slot = (int32_t)(e->retrim_gen % 3);
         rt_count = e->retrim_ring + rt_slot;
         ++e->retrim_gen;
-        if (e->retrim_chain != key) HIP_TRY(hipMemsetAsync(rt_count, 0, sizeof(int32_t), s));
+        if (e->retrim_chain != key || eager_after_capture) HIP_TRY(hipMemsetAsync(rt_count, 0, sizeof(int32_t), s));
         e->retrim_chain = key;
     }
     StepArgs a;
@@ -1428,8 +1450,8 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
         return fail(HG_E_INVALID, "actions/obs/reward/terminated/truncated must be device pointers");
     if (((uintptr_t)actions & 15) || ((uintptr_t)obs & 15))
         return fail(HG_E_INVALID, "actions and obs must be 16-byte aligned");
-    if (e->Pf.reset_retrim)
-        return fail(HG_E_INVALID, "hg_rollout does not support reset_mode RETRIM (re-trims run between steps)");
+    if (e->Pf.reset_retrim && e->Pf.autoreset)
+        return fail(HG_E_INVALID, "hg_rollout does not support auto-resets in reset_mode RETRIM (re-trims run between steps)");
     e->chain_expect = kChainBroken;
     StepArgs a;
     memset(&a, 0, sizeof(a));

@@ -160,6 +160,16 @@ struct Params {
     // Dryden wind (wind_dynamics.py:21-83)
     R wm[3], wind_dir_cos, wind_dir_sin, w20, sigma_low, turb_level, eta_norm;
     R tep_row[13];   // TEP table interpolated at turb_level, per altitude key (tep_row_values)
+    // folded products of the constants above for the packed fp32 step (stage_f32.h)
+    R f_kc_irho, f_og_irho;              // KC = K1 + f_kc_irho / rho; og = f_og_irho / rho (:214-220)
+    R f_mr_inflow_thr, f_tr_inflow_thr;  // inflow * coef / (2 pi R^2): the inflow ODE's thrust term per (wb - vi)
+    R f_mr_ct_k;                         // CT = max((wb - vi) * f_mr_ct_k, 0)
+    R f_mr_db_a, f_mr_db_b;              // DB1DV = f_mr_db_a CT + sqrt(f_mr_db_b CT)
+    R f_hXUU, f_hYVV, f_hZWW, f_zd;      // 0.5 XUU, 0.5 YVV, 0.5 ZWW; -0.5 ZWW COR (fuselage downwash moment)
+    R f_m2_R;                            // -2 / R_MR (H-tail downwash factor)
+    R f_rho_lz;                          // rho_exp * lapse / T0 (d ln rho / dz = f_rho_lz / (1 + lapse/T0 z))
+    R f_gyro[6];                         // I^-1 (pqr x I pqr) coefficients: p', r' of pq, qr; q' of pr, r^2 - p^2
+    R f_dpsi_mr, f_dpsi_tr;              // dt * Omega (rotor azimuth per step; runtime: depends on dt)
     // task (helicopter.py:63-68, helicopter_with_tasks.py)
     R n_t, n_t2, inv_n_x, inv_n_v, inv_n_a, tgt_n[3], vel_tgt_n, dwn_tgt_n;
     R fail_zdot, fail_ang;

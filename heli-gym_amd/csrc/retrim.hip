@@ -216,7 +216,8 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
     const int l = threadIdx.x;
     const hg::Params<double>& P = *a.P;
     const double eps = hg::kTrimEps;
-    const int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
+    int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
+    if (a.count && jobs > a.n) jobs = a.n;   // a queue holds at most one job per env
     for (int64_t job = blockIdx.x; job < jobs; job += gridDim.x) {   // uniform per wave
         const int64_t env = a.list ? (int64_t)a.list[job] : job;
         const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];

@@ -1,0 +1,396 @@
+// stage_f32.h — the fp32 step's helicopter RK4 (dynamics.py:158-171 over
+// HelicopterDynamics.dynamics, helicopter_dynamics.py:400-489), written for gfx950 issue.
+//
+// physics.h states the model once for both precisions and is what the fp64 trims run; this file
+// is the same model for the fp32 step kernel only, rearranged so that a lone wave (one wave per
+// SIMD at 65 536 envs) issues as few instructions as possible:
+//  * Packed fp32.  A wave alone issues one VALU instruction per ~4-5 cycles whether it is v_fma_f32
+//    or v_pk_fma_f32 (two fmas), so every pair of like operations is written as a 2-vector: the
+//    main and tail rotor's inflow / thrust / power (:203-300), the horizontal and vertical tail's
+//    stall branches (:322-361), the flapping equations (:236-262), the plane rotations of the DCM
+//    (kinematic.py:3-17), the RK4 combinations.  The stage state is held as pairs
+//    (vi_mr, vi_tr) (b0, b1) (u, v) (w, z) (p, q) (r, theta) (phi, psi) (x, y); the rotor
+//    azimuths, which no force model reads, advance by dt * Omega once per step.
+//  * Work moved out of the stages.  The ISA density (:160-165) and the main rotor's density
+//    terms (the flapping time constants ITB, ITB2_OM, :214-221) are evaluated once per step at the
+//    committed altitude z0 and linearised in z - z0 (the stage altitudes differ from z0 by
+//    dt * |w|: the quadratic term is below 1e-9 relative for |z - z0| < 1 ft, under half an fp32
+//    ulp at 10 ft).  Thrust over density (:246 T / (2 pi rho R^2)) and the thrust coefficient
+//    (:252) use (wb - vi) * coef directly: the density cancels.  The fuselage's downwash moment
+//    Z_F * d_fw (:305-318) is formed as -rho/2 ZWW COR |wa_f| (ua k + c wa_f): no division, and its
+//    limit 0 at wa_f = 0 comes out by itself.
+//  * Branches.  The H/V-tail stall selections are selects over both (packed) forms; the landing
+//    gear (:385-398) and the wing (:363-383) run only in wave-uniform branches and add their loads
+//    into the totals there, so a wave off the ground with no wing pays nothing for them.
+// Every rearrangement is exact in real arithmetic; the results differ from physics.h's fp32 form by
+// rounding only (the parity tests hold both to the same contract against the reference).
+#pragma once
+
+#include "physics.h"
+
+namespace hg {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// The stage state / derivative as pairs.
+struct X16 {
+    f2 vi;   // vi_mr, vi_tr
+    f2 b;    // b0, b1 (betas)
+    f2 uv;   // u, v
+    f2 wz;   // w, z
+    f2 pq;   // p, q
+    f2 rt;   // r, theta
+    f2 pp;   // phi, psi
+    f2 xy;   // x, y
+};
+
+// Everything the four stage evaluations of one step share.
+struct StepCtx {
+    f2 wb0, wb1;          // control-only parts of the blade inflow (mr_wb0, tr_vb0), (mr_wb1, tr_vb1)
+    f2 lon_lat, mlat_lon; // cyclic controls (rad): (lon, lat), (-lat, lon)
+    float W0, W1, W2;     // wind NED (set_wind, :156-158)
+    float z0;             // committed altitude coordinate (the density expansion point)
+    f2 ri0, riz;          // (rho, 1/rho) at z0 and their z-derivatives
+    f2 itb0, itbz;        // (-ITB2_OM, ITB) at z0 and their z-derivatives
+    float cz;             // the gear cannot touch while z < cz (committed-ground bound, conservative)
+    Ground<float> g;      // ground under the committed x, y (F6)
+};
+
+// (sin, cos) of the three attitude angles
+struct Att2 {
+    f2 a[3];
+};
+
+HD f2 sincos2(float x) {
+    float s, c;
+    m_sincos(x, &s, &c);
+    return f2{s, c};
+}
+
+// The step's shared part: controls (:414-422 + the control terms of :226, :281), the density
+// expansion at the committed altitude, the gear-contact bound.
+HD StepCtx step_ctx(const Params<float>& P, float a0, float a1, float a2, float a3, float W0, float W1, float W2,
+                    const Ground<float>& g, float z0) {
+    StepCtx c;
+    const float coll = P.coll0 + P.coll1 * a0;
+    const float lon = P.lon0 + P.lon1 * a1;
+    const float lat = P.lat0 + P.lat1 * a2;
+    c.lon_lat = f2{lon, lat};
+    c.mlat_lon = f2{-lat, lon};
+    const float ped = P.ped0 + P.ped1 * a3;
+    c.wb0 = f2{P.mr_two3_vtip, P.tr_two3_vtip} * (f2{coll, ped} + f2{P.mr_tw75, P.tr_tw75});
+    c.wb1 = f2{P.mr_inv_VTIP, P.tr_inv_VTIP} * (f2{coll, ped} + f2{P.mr_tw50, P.tr_tw50});
+    c.W0 = W0;
+    c.W1 = W1;
+    c.W2 = W2;
+    c.g = g;
+    c.z0 = z0;
+    // ISA density rho(z) = RO_SEA (1 + l z)^e (:160-165) and d rho / dz = rho e l / (1 + l z)
+    const float base = 1.f + P.lapse_t0 * z0;
+    const float rho = P.ro_sea * m_exp2(P.rho_exp * m_log2(base));
+    const float irho = m_rcp(rho);
+    const float rz = rho * P.f_rho_lz * m_rcp(base);
+    c.ri0 = f2{rho, irho};
+    c.riz = f2{rz, -rz * irho * irho};
+    // flapping time constants (:214-221): og = OM igam, ITB2_OM = OM / (1 + og^2), ITB = ITB2_OM og
+    const float og = P.f_og_irho * irho;
+    const float iD = m_rcp(1.f + og * og);
+    const float itb2 = P.mr_OMEGA * iD;
+    const float itb = itb2 * og;
+    const float dog = P.f_og_irho * c.riz.y;            // d og / dz
+    const float ditb2 = -2.f * itb2 * og * dog * iD;    // d ITB2_OM / dz
+    c.itb0 = f2{-itb2, itb};
+    c.itbz = f2{-ditb2, ditb2 * og + itb2 * dog};
+    // a gear point's pos_z + h is at most zh + lg_reach (see tail_loads), zh = z + h
+    c.cz = -P.wl_cg_ft - P.lg_reach - g.h();
+    return c;
+}
+
+// Attitude of a stage from the committed one by the angle-addition formulas (physics.h
+// attitude_step), on (sin, cos) pairs; a wave with a large stage increment takes the full sincos.
+HD Att2 att_step(const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
+    const f2 d01 = pp - pp0;   // phi, psi increments
+    const float d2 = th - th0;
+    // sin d = d - d^3/6, cos d = 1 - d^2/2 + d^4/24 (|d| <= 0.05: within 2.7e-9 / 2.2e-11)
+    const f2 q01 = d01 * d01;
+    const f2 sd01 = d01 + (d01 * q01) * (-1.f / 6.f);
+    const f2 cd01 = 1.f + q01 * (-0.5f + q01 * (1.f / 24.f));
+    const float q2 = d2 * d2;
+    const float sd2 = d2 + (d2 * q2) * (-1.f / 6.f);
+    const float cd2 = 1.f + q2 * (-0.5f + q2 * (1.f / 24.f));
+    // (sin, cos)(e + d) = (s, c) cd + (c, -s) sd
+    const f2 A0 = a0.a[0], A1 = a0.a[1], A2 = a0.a[2];
+    Att2 a;
+    a.a[0] = A0 * cd01.x + f2{A0.y, -A0.x} * sd01.x;
+    a.a[1] = A1 * cd2 + f2{A1.y, -A1.x} * sd2;
+    a.a[2] = A2 * cd01.y + f2{A2.y, -A2.x} * sd01.y;
+    // a lane with a larger increment (a tumbling env) takes the full sincos, in a wave-uniform branch
+    const bool small = m_fabs(d01.x) <= 0.05f && m_fabs(d01.y) <= 0.05f && m_fabs(d2) <= 0.05f;
+#ifndef HG_ISA_HOT   // (analysis builds only: the hot path without its cold branches)
+    if (wave_any(!small)) {
+#else
+    if (false) {
+#endif
+        if (!small) {
+            a.a[0] = sincos2(pp.x);
+            a.a[1] = sincos2(th);
+            a.a[2] = sincos2(pp.y);
+        }
+    }
+    return a;
+}
+
+// One evaluation of the model at stage state s (helicopter_dynamics.py:400-489) -> derivatives k;
+// with OBS also the 17 observations (:471-488) and the total power.
+template <bool OBS>
+HD void stage_f32(const Params<float>& P, const StepCtx& c, const X16& s, const Att2& at, X16& k,
+                  float* __restrict__ obs) {
+#ifdef HG_ISA_MARKS
+    asm volatile("; HGMARK stage begin");
+#endif
+    const float u = s.uv.x, v = s.uv.y, w = s.wz.x, z = s.wz.y, p = s.pq.x, q = s.pq.y, r = s.rt.x;
+    const f2 SC0 = at.a[0], SC1 = at.a[1], SC2 = at.a[2];
+    const float s0 = SC0.x, c0 = SC0.y, s1 = SC1.x, c1 = SC1.y, s2 = SC2.x, c2 = SC2.y;
+
+    // ---- kinematics (kinematic.py:3-29, :423-431).  Rotations are written so that every sign
+    // flip and lane swap is an operand modifier of the packed instruction: (s, c).yx * (x, -x) etc.
+    const float ic1 = m_rcp(c1);
+    const f2 sqth = SC0 * q + SC0.yx * f2{r, -r};              // (s0 q + c0 r, theta')
+    const float phid = p + (s1 * ic1) * sqth.x, psid = ic1 * sqth.x;
+    // NED velocity B^T uvw = Rz^T Ry^T Rx^T uvw
+    const f2 yz1 = SC0.yx * v + SC0 * f2{-w, w};                 // Rx^T (y, z)
+    const f2 xz2 = SC1.yx * f2{u, -u} + SC1 * yz1.y;           // Ry^T (x, z)
+    const f2 n01 = SC2.yx * xz2.x - SC2 * f2{yz1.x, -yz1.x};   // Rz^T (x, y)
+    const float n2 = xz2.y;
+    // air-relative body velocity uvw - B W, B = Rx Ry Rz
+    const f2 ab = SC2.yx * f2{c.W0, -c.W0} + SC2 * c.W1;       // Rz W (x, y)
+    const f2 xg = SC1.yx * ab.x + SC1 * f2{-c.W2, c.W2};       // Ry (x, z)
+    const f2 yzw = SC0 * xg.y + SC0.yx * f2{ab.y, -ab.y};      // Rx (y, z)
+    const float ua = u - xg.x;
+    const f2 vwa = f2{v, w} - yzw;
+    const float va = vwa.x, wa = vwa.y;
+    const f2 B12 = SC0 * c1;                                   // (B12, B22); B02 = -s1
+
+    // ---- density and the main rotor's density terms, linear in z - z0 (see the file comment)
+    const float dz = z - c.z0;
+    const f2 ri = c.ri0 + c.riz * dz;
+    const float rho = ri.x, irho = ri.y;
+    const f2 itb = c.itb0 + c.itbz * dz;                       // (-ITB2_OM, ITB)
+
+    // ---- main rotor (:203-270) and tail rotor (:272-300), packed as (MR, TR)
+    const f2 B = s.b;
+    const f2 BM = B - f2{P.mr_IS, 0.f};                        // (b0 - IS, b1)
+    const float ua2 = ua * ua;
+    const float wr = wa + BM.x * ua - BM.y * va;               // (:222-224)
+    const float wq = wa + q * P.tr_D;                          // (:276-279)
+    const float vr = -(va - r * P.tr_D + p * P.tr_H);
+    const f2 vav = f2{va, wq};
+    const f2 vadv = vav * vav + ua2;                           // (ua^2 + va^2, wq^2 + ua^2)
+    const f2 wrvr = f2{wr, vr};
+    const f2 wb = wrvr + c.wb0 + vadv * c.wb1;                 // blade-relative inflow (:226, :281)
+    const f2 dth = wb - s.vi;                                  // thrust = dth rho coef (:246, :284)
+    const f2 thr = dth * (rho * f2{P.mr_coef, P.tr_coef});
+    const f2 dw = wrvr - s.vi;
+    const f2 sq = dw * dw + vadv;
+    const f2 sr = f2{m_sqrt(sq.x), m_sqrt(sq.y)};
+    // inflow ODEs (:247-249, :285-286)
+    const f2 dvi = dth * f2{P.f_mr_inflow_thr, P.f_tr_inflow_thr} - f2{P.mr_inflow, P.tr_inflow} * (s.vi * sr);
+    const f2 pw = thr * dw;                                    // -(induced power) of each rotor (:250, :292)
+    const float power_mr = rho * P.mr_prof * (P.mr_vtip2 + 3.f * vadv.x) - pw.x;
+    const float power_tr = -pw.y;
+    // flapping (:228-262)
+    float CT = dth.x * P.f_mr_ct_k;
+    CT = CT > 0.f ? CT : 0.f;
+    const float DB1DV = P.f_mr_db_a * CT + m_sqrt(P.f_mr_db_b * CT);
+    const bool wake = m_fabs(ua) > P.vtrans;
+    const float f1 = wake ? 2.f : 1.f, f3n = wake ? -3.f : -1.f;
+    const float KC = P.mr_K1 + P.f_kc_irho * irho;
+    // (a_sum, b_sum) = (b1 - lat + KC b0 + DB1DV va f1, b0 + lon - KC b1 - DB1DV ua f3)
+    const f2 absum = (B.yx + c.mlat_lon) + B * f2{KC, -KC} + DB1DV * f2{va * f1, ua * f3n};
+    // (b0', b1') = (-ITB2_OM a_sum - ITB b_sum - q, ITB2_OM b_sum - ITB a_sum - p)
+    const f2 dB = absum * f2{itb.x, -itb.x} - (absum.yx * itb.y + s.pq.yx);
+    // forces and moments of the main rotor (:264-269): (X, Y) = -T (b0 - IS, -b1), Z = -T
+    const f2 XYn = BM * f2{thr.x, -thr.x};                     // -(X_MR, Y_MR)
+    const float DL_DA1 = rho * P.mr_DL_DA1_dro;
+    // (b0 + lon - K1 b1, lat - b1 - K1 b0)
+    const f2 inner = B * f2{1.f, -1.f} + c.lon_lat - P.mr_K1 * B.yx;
+    // (L, M) = H (Y, -X) + DL_DB1 (b1, b0) + DL_DA1 inner
+    const f2 LM_MR = XYn.yx * f2{-P.mr_H, P.mr_H} + P.mr_DL_DB1 * B.yx + DL_DA1 * inner;
+
+    // ---- fuselage (:302-320)
+    const float wa_f0 = wa - s.vi.x;
+    const float wa_f = wa_f0 > 0.f ? wa_f0 + (float)kEps : wa_f0;
+    const f2 XY_F = (rho * f2{P.f_hXUU, P.f_hYVV}) * f2{m_fabs(ua) * ua, m_fabs(va) * va};
+    const float awf = m_fabs(wa_f);
+    const float Z_F = rho * P.f_hZWW * (awf * wa_f);
+    const float zd = rho * P.f_zd * awf * (ua * P.fus_dfw_k + P.fus_dfw_c * wa_f);   // Z_F d_fw
+    const float power_fus = -(XY_F.x * ua + XY_F.y * va + Z_F * wa_f);
+    const float p_extra = power_fus - P.wt * n2;                 // + climb power (:435, :446-447)
+
+    // ---- horizontal (:322-345) and vertical (:347-361) tail, packed as (HT, VT)
+    const float v_dw = m_max(-wa_f0, (float)kEps);
+    const float d_dw = ua * m_rcp(v_dw) * P.ht_dw_k - P.ht_dw_c;
+    const float eps_ht = (d_dw > 0.f && d_dw < P.mr_R) ? 2.f + d_dw * P.f_m2_R : 0.f;
+    const float wa_ht = wa - eps_ht * s.vi.x + P.ht_D * q;
+    const float va_vt = va + s.vi.y - P.vt_D * r;
+    const f2 X = f2{wa_ht, va_vt};
+    const float aua = m_fabs(ua);
+    const f2 S2 = X * X + f2{vadv.x, ua2};
+    const f2 stall = f2{P.ht_ZMAX, P.vt_YMAX} * f2{m_sqrt(S2.x), m_sqrt(S2.y)} * X;
+    const f2 lin = (f2{P.ht_ZUU, P.vt_YUU} * ua + f2{P.ht_ZUW, P.vt_YUV} * X) * aua;
+    const float lim = 0.3f * aua;
+    const f2 ZY = (0.5f * rho) * f2{m_fabs(wa_ht) > lim ? stall.x : lin.x, m_fabs(va_vt) > lim ? stall.y : lin.y};
+
+    // ---- totals (:446-459)
+    float Fx = XY_F.x - XYn.x - P.wt * s1;
+    f2 Fyz = f2{XY_F.y - XYn.y, Z_F - thr.x} + f2{thr.y + ZY.y, ZY.x} + P.wt * B12;
+    float Mx = LM_MR.x + XY_F.y * P.fus_H + thr.y * P.tr_H + ZY.y * P.vt_H;
+    float My = LM_MR.y + (zd - XY_F.x * P.fus_H) + ZY.x * P.ht_D - thr.x * P.mr_D;
+    const float pmain = power_mr + p_extra;
+    float Mz = pmain * P.mr_inv_OMEGA - thr.y * P.tr_D - ZY.y * P.vt_D;
+    float power = pmain + power_tr;
+    // wing (:363-383); the AW109 has none (uniform branch)
+    if (P.wn_on) {
+        const float wa_w = wa - s.vi.x;
+        const float vta2 = ua * ua + wa_w * wa_w;
+        const float qq = P.wn_ZUU * ua * ua + P.wn_ZUW * ua * wa_w;
+        const float rh = 0.5f * rho;
+        const float Z_WN = m_fabs(wa_w) > lim ? rh * P.wn_ZMAX * m_sqrt(vta2) * wa_w : rh * qq;
+        const float X_WN = -rh * (float)(1.0 / kPi) * m_rcp(vta2) * qq * qq;
+        Fx += X_WN;
+        Fyz.y += Z_WN;
+        power += m_fabs(X_WN * ua);
+    }
+    // landing gear (:385-398), only where some lane of the wave may touch.  QUIRK: the moment uses
+    // the ACCUMULATED force (:397).
+#ifndef HG_ISA_HOT
+    if (wave_any(z > c.cz)) {
+#else
+    if (false) {
+#endif
+        const float zh = c.g.zh(z);
+        const f2 B22 = B12;
+        float Fl0 = 0.f, Fl1 = 0.f, Fl2 = 0.f, Ml0 = 0.f, Ml1 = 0.f, Ml2 = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi) {
+            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
+            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
+            if (-pzh - P.wl_cg_ft < 0.f) {
+                const float cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
+                const float vel_z = n2 + (-s1 * cx + B22.x * cy + B22.y * cz);
+                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
+                Fl0 += -s1 * fz; Fl1 += B22.x * fz; Fl2 += B22.y * fz;
+                Ml0 += ry * Fl2 - rz * Fl1;
+                Ml1 += rz * Fl0 - rx * Fl2;
+                Ml2 += rx * Fl1 - ry * Fl0;
+            }
+        }
+        Fx += Fl0;
+        Fyz += f2{Fl1, Fl2};
+        Mx += Ml0;
+        My += Ml1;
+        Mz += Ml2;
+    }
+
+    // ---- equations of motion (:448-470)
+    // uvw' = F / m - pqr x uvw
+    const f2 duv = f2{Fx, Fyz.x} * P.inv_mass + r * f2{v, -u} + w * f2{-q, p};
+    const float dw_ = Fyz.y * P.inv_mass + (q * u - p * v);
+    // pqr' = I^-1 (M - pqr x I pqr), I = [[Ixx,0,Ixz],[0,Iyy,0],[Ixz,0,Izz]]: the gyroscopic term is
+    // (Ixz pq + (Izz-Iyy) qr, (Ixx-Izz) pr + Ixz (r^2 - p^2), (Iyy-Ixx) pq - Ixz qr) and I^-1 couples
+    // p and r only, so (p', r') = J0 Mx + J2 Mz + Cpq pq + Cqr qr, q' = Ji11 My + Cpr pr + Crr (r^2 - p^2)
+    // with the coefficients folded on the host (derive: f_gyro)
+    const float pq_ = p * q;
+    const f2 qrpr = s.pq.yx * r;                               // (q r, p r)
+    const float rrpp = r * r - p * p;
+    const f2 dpr = f2{P.Ji00, P.Ji20} * Mx + f2{P.Ji02, P.Ji22} * Mz + f2{P.f_gyro[0], P.f_gyro[1]} * pq_ +
+                   f2{P.f_gyro[2], P.f_gyro[3]} * qrpr.x;
+    const float dq = P.Ji11 * My + P.f_gyro[4] * qrpr.y + P.f_gyro[5] * rrpp;
+    k.vi = dvi;
+    k.b = dB;
+    k.uv = duv;
+    k.wz = f2{dw_, n2};
+    k.pq = f2{dpr.x, dq};
+    k.rt = f2{dpr.y, sqth.y};
+    k.pp = f2{phid, psid};
+    k.xy = n01;
+    if (OBS) {   // the observation at this stage's input state (:471-488)
+        obs[0] = (power + P.p_loss) * (float)(1.0 / 550.0);
+        obs[1] = ua; obs[2] = va; obs[3] = wa;
+        obs[4] = n01.x; obs[5] = n01.y; obs[6] = n2;
+        obs[7] = s.pp.x; obs[8] = s.rt.y; obs[9] = s.pp.y;
+        obs[10] = p; obs[11] = q; obs[12] = r;
+        obs[13] = s.xy.x; obs[14] = s.xy.y; obs[15] = -z; obs[16] = -c.g.zh(z);
+    }
+}
+
+// RK combinations on the pairs (dynamics.py:166-168): st = hs + h k, acc (+)= (2) k
+template <bool FIRST>
+HD void rk_stage2(const X16& hs, const X16& k, X16& acc, X16& st, float h) {
+#define HG_RK_PAIR(f)                                   \
+    acc.f = FIRST ? k.f : acc.f + 2.f * k.f;            \
+    st.f = hs.f + k.f * h;
+    HG_RK_PAIR(vi) HG_RK_PAIR(b) HG_RK_PAIR(uv) HG_RK_PAIR(wz) HG_RK_PAIR(pq) HG_RK_PAIR(rt) HG_RK_PAIR(pp)
+    HG_RK_PAIR(xy)
+#undef HG_RK_PAIR
+}
+
+HD void rk_update2(X16& hs, const X16& k, const X16& acc, float dt6) {
+#define HG_RK_UPD(f) hs.f = hs.f + (acc.f + k.f) * dt6;
+    HG_RK_UPD(vi) HG_RK_UPD(b) HG_RK_UPD(uv) HG_RK_UPD(wz) HG_RK_UPD(pq) HG_RK_UPD(rt) HG_RK_UPD(pp) HG_RK_UPD(xy)
+#undef HG_RK_UPD
+}
+
+HD X16 to_x16(const float* s) {
+    X16 x;
+    x.vi = f2{s[0], s[1]};
+    x.b = f2{s[4], s[5]};
+    x.uv = f2{s[6], s[7]};
+    x.wz = f2{s[8], s[17]};
+    x.pq = f2{s[9], s[10]};
+    x.rt = f2{s[11], s[13]};
+    x.pp = f2{s[12], s[14]};
+    x.xy = f2{s[15], s[16]};
+    return x;
+}
+
+HD void from_x16(const X16& x, float* s) {   // (s[2], s[3], the rotor azimuths, are not in X16)
+    s[0] = x.vi.x; s[1] = x.vi.y;
+    s[4] = x.b.x; s[5] = x.b.y;
+    s[6] = x.uv.x; s[7] = x.uv.y;
+    s[8] = x.wz.x; s[17] = x.wz.y;
+    s[9] = x.pq.x; s[10] = x.pq.y;
+    s[11] = x.rt.x; s[13] = x.rt.y;
+    s[12] = x.pp.x; s[14] = x.pp.y;
+    s[15] = x.xy.x; s[16] = x.xy.y;
+}
+
+// One RK4 step of the 18-state model (dynamics.py:158-171): hs advanced in place, k4 (the
+// reference's state_dots, what the reward reads) in d, the stage-4 observation in obs.
+HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,
+                     float* __restrict__ obs) {
+    X16 h = to_x16(hs);
+    Att2 a0;
+    a0.a[0] = sincos2(h.pp.x);
+    a0.a[1] = sincos2(h.rt.y);
+    a0.a[2] = sincos2(h.pp.y);
+    X16 k, acc, st;
+    stage_f32<false>(P, c, h, a0, k, obs);
+    rk_stage2<true>(h, k, acc, st, P.half_dt);
+    stage_f32<false>(P, c, st, att_step(a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    rk_stage2<false>(h, k, acc, st, P.half_dt);
+    stage_f32<false>(P, c, st, att_step(a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    rk_stage2<false>(h, k, acc, st, P.dt);
+    stage_f32<true>(P, c, st, att_step(a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    rk_update2(h, k, acc, P.dt6);
+    from_x16(h, hs);
+    // rotor azimuths: constant rates (:457-458), dt / 6 (O + 2 O + 2 O + O) = dt O
+    const f2 psi = f2{hs[2], hs[3]} + f2{P.f_dpsi_mr, P.f_dpsi_tr};
+    hs[2] = psi.x;
+    hs[3] = psi.y;
+    from_x16(k, d);
+    d[2] = P.mr_OMEGA;
+    d[3] = P.tr_OMEGA;
+}
+
+}  // namespace hg

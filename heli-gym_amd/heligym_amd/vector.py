@@ -79,6 +79,45 @@ class LazyInfo(dict):
     def copy(self):
         return {k: self._get(k) for k in list(dict.keys(self))}
 
+    # every other read path goes through _get as well, so no caller ever sees a None placeholder
+    def __setitem__(self, k, v):
+        self._pending.discard(k)
+        dict.__setitem__(self, k, v)
+
+    def update(self, *args, **kw):
+        for k, v in dict(*args, **kw).items():
+            self[k] = v
+
+    _MISSING = object()
+
+    def pop(self, k, default=_MISSING):
+        if k not in self:
+            if default is LazyInfo._MISSING:
+                raise KeyError(k)
+            return default
+        v = self._get(k)
+        dict.pop(self, k)
+        return v
+
+    def popitem(self):
+        if not len(self):
+            raise KeyError("popitem(): dictionary is empty")
+        k = list(dict.keys(self))[-1]
+        return k, self.pop(k)
+
+    def setdefault(self, k, default=None):
+        if k in self:
+            return self._get(k)
+        dict.__setitem__(self, k, default)
+        return default
+
+    def __reduce__(self):   # pickles / deep-copies as the plain dict of its values
+        return (dict, (self.copy(),))
+
+    def __deepcopy__(self, memo):
+        import copy
+        return copy.deepcopy(self.copy(), memo)
+
     def __repr__(self):
         return repr(self.copy())
 
@@ -308,6 +347,10 @@ class HeliVecEnv(*_VEC_BASES):
         p = b["p"]
         rs = with_reset_info and self.autoreset and self.autoreset_mode == "same_step"
         g = self._gen
+        if not rs or rows:
+            # only a compacted step (step_async with reset info) fills these; after any other step
+            # they would hold another step's data
+            self.reset_count = self.reset_index = self.final_obs = None
         if rs and rows:
             rc = self.lib.hg_step_rows(self._h, a.data_ptr(), p_obs, self._p_rew, self._p_term, self._p_trunc, p[0],
                                        None if e is None else e.data_ptr(), p[2], self._stream())

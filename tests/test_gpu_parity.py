@@ -522,6 +522,60 @@ def test_reset_count_across_consecutive_launches(torch, n):
     env.close()
 
 
+@pytest.mark.parametrize("mode", ["template", "retrim"])
+def test_reset_count_eager_capture_replay_interleaved(torch, mode):
+    """Back-to-back chained steps (step_async with reset info, no other launch between) and the
+    sequence eager -> capture -> eager -> replay -> eager -> replay, with resets in every step: the
+    host never sees a replay, so an eager step after any capture must not trust that its ring slot
+    was zeroed.  Each eager step's count and index set equal its done flags; every replay's too; the
+    re-trim queue never re-trims an env that did not reset (mid-episode rows stay bitwise those of a
+    twin that never ran a graph)."""
+    n = 1000
+    env = make_env(torch, n, "hover", 0.01, autoreset=True, max_episode_steps=3, reset_mode=mode)
+    env.reset()
+    st, ctr = env.get_state()
+    ctr[:, 0] = torch.arange(n, device=env.device, dtype=torch.int32) % 3
+    env.set_state(st, ctr)
+    act = torch.zeros((n, 4), device=env.device)
+
+    def eager(steps):
+        for _ in range(steps):
+            env.step_async(act)
+            done = (env.terminated_u8 | env.truncated_u8).cpu().numpy()
+            k = int(env.reset_count.item())
+            assert k == done.sum(), (mode, k, done.sum())
+            np.testing.assert_array_equal(np.sort(env.reset_index[:k].cpu().numpy()), np.nonzero(done)[0])
+
+    eager(5)   # back to back: each kernel zeroes the next step's slot
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        env.step_async(act)
+    cnt_t, idx_t = env.reset_count, env.reset_index
+    eager(2)
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        done = (env.terminated_u8 | env.truncated_u8).cpu().numpy()
+        k = int(cnt_t.item())
+        assert k == done.sum(), (mode, "replay")
+        np.testing.assert_array_equal(np.sort(idx_t[:k].cpu().numpy()), np.nonzero(done)[0])
+        eager(1)   # the slot after a replay: zeroed by this launch, not assumed zero
+    assert env.retrim_failures() == 0
+    # 5 + 1 (the capture does not run) + 2 + 2 * 2 = 11 steps; a twin stepped 11 times eagerly, never
+    # capturing, must hold the same state bitwise (a stray re-trim of a mid-episode env would not)
+    s_got, c_got = env.get_state()
+    twin = make_env(torch, n, "hover", 0.01, autoreset=True, max_episode_steps=3, reset_mode=mode)
+    twin.reset()
+    twin.set_state(st, ctr)
+    for _ in range(11):
+        twin.step_async(act)
+    s_ref, c_ref = twin.get_state()
+    np.testing.assert_array_equal(c_got.cpu().numpy(), c_ref.cpu().numpy())
+    np.testing.assert_array_equal(s_got.cpu().numpy().view(np.uint32), s_ref.cpu().numpy().view(np.uint32))
+    twin.close()
+    env.close()
+
+
 def test_setters_match_reference_semantics(torch, terrain_u16):
     """set_trim_cond / set_target / set_max_time (helicopter.py:89-106) through the batched env:
     the reset state is the re-trimmed one, the reward uses the new target, and `truncated` rises on

@@ -57,3 +57,29 @@ def test_read_after_reuse_raises_but_cached_values_stay():
         info["b"]
     with pytest.raises(_abi.HeliGymError):
         info.copy()
+
+
+def test_mutating_reads_never_return_placeholders():
+    """pop / popitem / setdefault / update / pickling go through the lazy read like __getitem__
+    (dict's own versions would hand out the None placeholder of an unread field)."""
+    import copy
+    import pickle
+    calls, valid = [], [True]
+    info, _ = make(valid, calls)
+    assert info.pop("b") == 20 and "b" not in info and calls == ["b"]
+    assert info.pop("b", 7) == 7
+    with pytest.raises(KeyError):
+        info.pop("b")
+    assert info.setdefault("a", 99) == 10 and info.setdefault("new", 3) == 3 and info["new"] == 3
+    k, v = info.popitem()
+    assert (k, v) == ("new", 3)
+    info.update(p0=-1)
+    assert info["p0"] == -1 and "p0" not in info._pending
+    assert pickle.loads(pickle.dumps(info)) == {"a": 10, "p0": -1, "p1": 2}
+    assert copy.deepcopy(info) == {"a": 10, "p0": -1, "p1": 2}
+    valid[0] = False
+    info2, _ = make(valid, [])
+    with pytest.raises(_abi.HeliGymError):
+        info2.pop("a")
+    with pytest.raises(_abi.HeliGymError):
+        info2.setdefault("a")
