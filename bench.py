@@ -112,10 +112,10 @@ def cpu_share():
 
 
 # ------------------------------------------------------------------------------------ references
-def pmc_traffic(envs, dt, task):
-    """HBM bytes per step-kernel launch from the newest committed PMC summary for this workload
-    (profiles/<tag>_pmc_summary.json, written by scripts/summarize_prof.py from rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes).  None if this workload was not profiled."""
+def pmc_summary(envs, dt, task, need="hbm_bytes_per_launch", tags=None):
+    """The newest committed PMC summary for this workload (profiles/<tag>_pmc_summary.json, written
+    by scripts/summarize_prof.py from rocprofv3 --pmc passes) that has `need`, as (dict, path), or
+    None.  Newest = last in tag order; `tags` restricts the search to those tags."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
@@ -123,10 +123,45 @@ def pmc_traffic(envs, dt, task):
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("envs") == envs and abs(d.get("dt", -1) - dt) < 1e-12 and d.get("task", "hover") == task \
-                and "hbm_bytes_per_launch" in d:
-            best = (d["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
+        if tags is not None and d.get("tag") not in tags:
+            continue
+        have = need in d or need in d.get("counters_per_launch", {})
+        if d.get("envs") == envs and abs(d.get("dt", -1) - dt) < 1e-12 and d.get("task", "hover") == task and have:
+            best = (d, os.path.relpath(f, ROOT))
     return best
+
+
+def pmc_traffic(envs, dt, task):
+    """HBM bytes per step-kernel launch (FETCH_SIZE / WRITE_SIZE passes), or None."""
+    r = pmc_summary(envs, dt, task)
+    return None if r is None else (r[0]["hbm_bytes_per_launch"], r[1])
+
+
+def shader_clock_ghz(dt, task, fallback_ghz):
+    """The shader clock under this kernel's load: GRBM_GUI_ACTIVE / 8 XCDs / kernel time of the
+    committed PMC summary of the out-of-cache workload (its ~0.27 ms dispatches are long enough for
+    that quotient, MI355X_MICROARCH.md DVFS note); else the device's maximum clock."""
+    r = pmc_summary(OUT_OF_CACHE_ENVS, dt, task, need="GRBM_GUI_ACTIVE")
+    if r is not None and r[0].get("kernel_avg_ns_trace"):
+        return r[0]["counters_per_launch"]["GRBM_GUI_ACTIVE"] / 8 / r[0]["kernel_avg_ns_trace"], r[1] + " (GRBM_GUI_ACTIVE / 8 / trace time)"
+    return fallback_ghz, "device maximum clock"
+
+
+def valu_issue(envs, dt, task, kern_s, simds, clock_ghz):
+    """The VALU issue ceiling beside the HBM one: VALU wave-instructions per
+    launch (SQ_INSTS_VALU of the committed PMC summary of this workload) x 4 cycles (a wave issues at
+    most one VALU instruction per ~4 cycles) / (SIMDs x clock x the live per-launch time)."""
+    r = pmc_summary(envs, dt, task, need="SQ_INSTS_VALU")
+    if r is None:
+        return None
+    c = r[0]["counters_per_launch"]
+    waves = c.get("SQ_WAVES") or 1.0
+    valu = c["SQ_INSTS_VALU"]
+    out = {"valu_issue_frac": valu * 4 / (simds * clock_ghz * 1e9 * kern_s),
+           "valu_per_wave": valu / waves, "salu_per_wave": c.get("SQ_INSTS_SALU", 0.0) / waves,
+           "valu_issue_source": f"{r[1]} (SQ_INSTS_VALU per launch) x 4 cycles / ({simds} SIMDs x "
+                                f"{clock_ghz:.3f} GHz x live kernel time)"}
+    return out
 
 
 def cpu_baseline(dt, task, seconds):
@@ -515,6 +550,26 @@ def main():
                     "note": "open-loop action sequences (planning / data generation); same results as "
                             "hg_step, state read and written once per launch"}
 
+        if world == 1 and not args.no_secondary and not args.dry_run and args.reset_mode == "template":
+            # the same workload with exact F8 resets: every auto-reset re-trimmed on the device against
+            # the env's last wind (reset_mode="retrim", helicopter.py:208-212)
+            envr = make_env(argparse.Namespace(**{**vars(args), "reset_mode": "retrim"}), torch, N, rank * N, dev)
+            Kr = min(K, 500)
+
+            def stepr(k):
+                envr.step_async(bank[k % B], with_reset_info=False)
+            for k in range(min(args.warmup, 50)):
+                stepr(k)
+            repr_, _kr = graphs_for(torch, dev, stepr, Kr, B)
+            s_rt, _, _ = timer.run(repr_, 3)
+            del _kr
+            secondary["retrim"] = {
+                "envs": N, "value": N * Kr / s_rt, "unit": "env-steps/s", "ms_per_step": s_rt / Kr * 1e3,
+                "steps": Kr, "retrim_failures": envr.retrim_failures(),
+                "note": "reset_mode='retrim': each step's auto-resets re-trimmed on the device (Newton trim "
+                        "against the env's last wind, the reference's reset from episode 2 on), hipGraph"}
+            envr.close()
+
         if world == 1 and not args.no_secondary and not args.dry_run and args.envs < OUT_OF_CACHE_ENVS:
             # the same step past the 256 MB Infinity Cache (1.39 GB moved per launch): HBM bytes, not
             # fabric bytes, with its own committed PMC summary
@@ -607,6 +662,18 @@ def main():
     if args.dry_run:
         out["dry_run"] = "plumbing check only: no kernel ran, nothing was measured"
         out["roofline"].update(achieved=None, frac=None)
+    else:
+        props = torch.cuda.get_device_properties(dev)
+        simds = 4 * props.multi_processor_count
+        ghz, ghz_src = shader_clock_ghz(args.dt, args.task, getattr(props, "clock_rate", 2400000) / 1e6)
+        vi = valu_issue(total_envs // world, args.dt, args.task, kern_s, simds, ghz)
+        if vi is not None:
+            out["roofline"].update(vi, clock_ghz=ghz, clock_source=ghz_src)
+        if "out_of_cache" in secondary:
+            oc = secondary["out_of_cache"]
+            vx = valu_issue(oc["envs"], args.dt, args.task, oc["ms_per_step"] * 1e-3, simds, ghz)
+            if vx is not None:
+                oc.update(vx)
     if args.gather_obs:
         out["roofline"]["kernel_avg_source"] = "timed window / steps (eager with gathers: an upper bound)"
     out.update(secondary)

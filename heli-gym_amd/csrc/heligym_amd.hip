@@ -25,7 +25,6 @@
 #include "trim.h"
 #include "retrim.h"
 #include "baked.h"
-#include "stage_f32.h"
 
 using hg::Params;
 using hg::Template;
@@ -59,7 +58,7 @@ constexpr int kBlock = 256;
 #define HG_STEP_BLOCK 64
 #endif
 constexpr int kStepBlock = HG_STEP_BLOCK;   // step kernel block: one or more waves, one state tile each
-static_assert(kTileEnvs % 64 == 0, "a state tile holds whole waves");
+static_assert(kTileEnvs == 64, "a state tile is one wave");
 constexpr int kStateCols = HG_STATE_COLS;
 constexpr int kCtrCols = HG_COUNTER_COLS;
 
@@ -69,9 +68,12 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
+#ifndef HG_PHILOX_ROUNDS
+#define HG_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < HG_PHILOX_ROUNDS; ++i) {
         const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
         const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
         c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
@@ -147,10 +149,21 @@ __device__ __forceinline__ void st_out(T* p, T v) {
     if constexpr (NT && sizeof(T) >= 4) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
+#ifndef HG_WT   // experiment: write-through (sc1) output stores, as pairs of 8-byte agent-scope stores
+#define HG_WT 0
+#endif
+__device__ __forceinline__ void st_wt8(void* p, uint64_t v) {
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <bool NT>
 __device__ __forceinline__ void st_out4(float* p, const float* s) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(s);
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+    if constexpr (HG_WT && NT) {
+        const uint64_t lo = __builtin_bit_cast(uint64_t, __builtin_shufflevector(v, v, 0, 1));
+        const uint64_t hi = __builtin_bit_cast(uint64_t, __builtin_shufflevector(v, v, 2, 3));
+        st_wt8(p, lo);
+        st_wt8(p + 2, hi);
+    } else if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
     else *reinterpret_cast<f32x4*>(p) = v;
 }
 
@@ -179,7 +192,14 @@ __device__ __forceinline__ T ld_lane(const T* __restrict__ base, uint32_t idx) {
 template <bool NT, typename T>
 __device__ __forceinline__ void st_lane(T* base, uint32_t idx, T v) {
     HG_GLOBAL T* p = (HG_GLOBAL T*)((HG_GLOBAL char*)base + idx * (uint32_t)sizeof(T));
-    if constexpr (NT && sizeof(T) >= 4) __builtin_nontemporal_store(v, p);
+    if constexpr (HG_WT && NT && sizeof(T) == 16) {
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        const u64x2 w = __builtin_bit_cast(u64x2, v);
+        __hip_atomic_store((HG_GLOBAL uint64_t*)p, (uint64_t)w.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((HG_GLOBAL uint64_t*)p + 1, (uint64_t)w.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (HG_WT && NT && sizeof(T) == 8) {
+        __hip_atomic_store((HG_GLOBAL uint64_t*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (NT && sizeof(T) >= 4) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
@@ -291,9 +311,21 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
         const int w_ = (int)(i >> 6);                                                           \
         if ((tid & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;                      \
     } while (0)
+// the same stamp from inside the RK driver (stage_f32.h), where only the hardware ids are in scope
+#define HG_STAGE_STAMP(j, ...)                                                                  \
+    do {                                                                                        \
+        asm volatile("" ::__VA_ARGS__);                                                         \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+        const int w_ = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);                    \
+        if ((threadIdx.x & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;              \
+    } while (0)
 #else
 #define TSTAMP(j, ...) do { } while (0)
 #endif
+
+}  // namespace
+#include "stage_f32.h"   // (after the timing macros: HG_STAGE_STAMP)
+namespace {
 
 // TASK: reward / success of the task; ETA: noise injected by the caller (else in-kernel Philox);
 // NT: streaming output stores (see st_out); FEAT: the optional features (reset-info compaction,
@@ -320,35 +352,43 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     const int64_t i = blk0 + tid;
     const int64_t n = n_p;
     const bool active = i < n;
-    // Addressing: this wave's state tile (64 envs x 30 columns, contiguous) from one uniform (SGPR)
-    // base at its middle column, so every column is an immediate offset (+-3.8 KB, inside the 13-bit
-    // field) of the same SGPR-base access with the lane's byte offset: no address arithmetic per
-    // column.  Lanes past the end of a ragged last tile step its padding and store nothing; for the
-    // caller's [N]-row buffers they read row blk0.
+    // Addressing: this wave's state tile (8 groups x 64 lanes x 16 bytes, contiguous, retrim.h) from
+    // one uniform (SGPR) base at its middle group, so every group is an immediate offset (-4 .. +3 KB,
+    // inside the 13-bit field) of the same SGPR-base access with the lane's byte offset: no address
+    // arithmetic per group.  Lanes past the end of a ragged last tile step its padding and store
+    // nothing; for the caller's [N]-row buffers they read row blk0.
     const uint32_t lo = (uint32_t)(active ? tid : 0);
     const uint32_t lt = (uint32_t)tid;
-#define COL(ptr, c) ((ptr) + ((c) - 15) * kTileEnvs)
-    float* st_b = state_p + (blk0 / kTileEnvs) * kTileWords + (blk0 % kTileEnvs) + 15 * kTileEnvs;
-    int32_t* ct_b = reinterpret_cast<int32_t*>(st_b);
+    f32x4* st_b = reinterpret_cast<f32x4*>(state_p + tile * kTileWords) + 4 * kTileEnvs;
+#define GRP(ptr, g) ((ptr) + ((g) - 4) * kTileEnvs)
 
 #if HG_TIMING
     if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][15] = __builtin_amdgcn_s_memrealtime();
 #endif
     TSTAMP(0, "v"(tid));
-    // Loads in the order they are needed: position (-> terrain texel address), counters (-> noise
-    // key), wind state and carry (-> wind step), then the heli state.
+    // reset template (heli[18] | carry[4] | obs[17]) one float per lane, requested with the state so
+    // that a reset costs no round trip at the end (and no late load is outstanding when the step
+    // ends: a load issued near the stage-4 code makes the compiler wait for it there)
+    const float tpl = lane < kTplFloats ? reinterpret_cast<const float*>(Tp)[lane] : 0.f;
+    // The state groups in the order they are needed (retrim.h slot table): position and step
+    // counter (-> terrain texel address, noise key), the rest of the key and the carry, the wind
+    // state (-> wind step), then the heli state.
     float hs[18], ws[5], carry[4];
-    hs[15] = ld_lane(COL(st_b, 15), lt);
-    hs[16] = ld_lane(COL(st_b, 16), lt);
-    int32_t step = ld_lane(COL(ct_b, kCtrCol0 + 0), lt), succ = ld_lane(COL(ct_b, kCtrCol0 + 1), lt),
-            epi = ld_lane(COL(ct_b, kCtrCol0 + 2), lt);
-#pragma unroll
-    for (int c = 0; c < 5; ++c) ws[c] = ld_lane(COL(st_b, 18 + c), lt);   // the wind step needs these
-#pragma unroll
-    for (int c = 0; c < 4; ++c) carry[c] = ld_lane(COL(st_b, 23 + c), lt);
-#pragma unroll
-    for (int c = 0; c < 18; ++c)   // ... and the heli state streams in behind the noise and wind work
-        if (c != 15 && c != 16) hs[c] = ld_lane(COL(st_b, c), lt);
+    int32_t step, succ, epi;
+    {
+        const f32x4 g0 = ld_lane(GRP(st_b, 0), lt), g1 = ld_lane(GRP(st_b, 1), lt), g2 = ld_lane(GRP(st_b, 2), lt),
+                    g3 = ld_lane(GRP(st_b, 3), lt), g4 = ld_lane(GRP(st_b, 4), lt), g5 = ld_lane(GRP(st_b, 5), lt),
+                    g6 = ld_lane(GRP(st_b, 6), lt);
+        const f32x2 g7 = ld_lane(reinterpret_cast<const f32x2*>(GRP(st_b, 7)), 2 * lt);
+        hs[15] = g0.x; hs[16] = g0.y; hs[17] = g0.z; step = __float_as_int(g0.w);
+        epi = __float_as_int(g1.x); succ = __float_as_int(g1.y); carry[3] = g1.z; carry[0] = g1.w;
+        carry[1] = g2.x; carry[2] = g2.y; ws[0] = g2.z; ws[1] = g2.w;
+        ws[2] = g3.x; ws[3] = g3.y; ws[4] = g3.z; hs[2] = g3.w;
+        hs[0] = g4.x; hs[1] = g4.y; hs[4] = g4.z; hs[5] = g4.w;
+        hs[6] = g5.x; hs[7] = g5.y; hs[8] = g5.z; hs[9] = g5.w;
+        hs[10] = g6.x; hs[11] = g6.y; hs[12] = g6.z; hs[13] = g6.w;
+        hs[14] = g7.x; hs[3] = g7.y;
+    }
     if (FEAT && blockIdx.x == 0 && tid == 0) {   // counters of a later step (rings of three)
         if (a.reset_count_next) *a.reset_count_next = 0;
         if (a.retrim_slot >= 0 && a.retrim_count) a.retrim_count[a.retrim_slot == 2 ? 0 : a.retrim_slot + 1] = 0;
@@ -380,7 +420,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
     const hg::StepCtx ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, W[0], W[1], W[2], h_c, hs[17]);
     float k[18], obs[17];
-    hg::rk4_step_f32(P, ctx, hs, k, obs);
+    hg::rk4_step_f32<NT>(P, ctx, hs, k, obs);   // NT: the launch is one wave per SIMD
 #if HG_EARLY_POST
     // the terrain texels under the post-step position (the flags' ground height), requested now so
     // that their latency hides behind the wraps and the reward
@@ -394,9 +434,6 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
         st_lane<false>(wb + 1, 3 * (uint32_t)tid, W[1]);
         st_lane<false>(wb + 2, 3 * (uint32_t)tid, W[2]);
     }
-    // reset template (heli[18] | carry[4] | obs[17]) one float per lane, fetched now so that its
-    // latency hides behind the reward / flag work and a reset costs no round trip at the end
-    const float tpl = lane < kTplFloats ? reinterpret_cast<const float*>(Tp)[lane] : 0.f;
     // step_after (helicopter_dynamics.py:73-77)
     // utils.py pi_bound, (x + pi) % 2pi - pi.  An angle already in [-pi, pi) is kept as is -- what
     // the reference's fp64 arithmetic returns to 1e-16, where the fp32 round trip through x + pi
@@ -535,24 +572,23 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     store_obs_wave<NT, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, a.obs, so, blk0, n, lane);
     }   // steps
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
-    st_b = state_p + (blk0 / kTileEnvs) * kTileWords + (blk0 % kTileEnvs) + 15 * kTileEnvs;
+    st_b = reinterpret_cast<f32x4*>(state_p + tile * kTileWords) + 4 * kTileEnvs;
     asm volatile("" : "+s"(st_b));
-    ct_b = reinterpret_cast<int32_t*>(st_b);
     if (active) {
         // the lane index re-materialised in this block, so that each store selects the SGPR-base
         // form (a 32-bit lane offset) instead of a 64-bit VALU address add per store
         uint32_t t = (uint32_t)tid;
         asm volatile("" : "+v"(t));
-#pragma unroll
-        for (int c = 0; c < 18; ++c) st_lane<NT>(COL(st_b, c), t, hs[c]);
-#pragma unroll
-        for (int c = 0; c < 5; ++c) st_lane<NT>(COL(st_b, 18 + c), t, ws[c]);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) st_lane<NT>(COL(st_b, 23 + c), t, carry[c]);
-        st_lane<NT>(COL(ct_b, kCtrCol0 + 0), t, step);
-        st_lane<NT>(COL(ct_b, kCtrCol0 + 1), t, succ);
-        st_lane<NT>(COL(ct_b, kCtrCol0 + 2), t, epi);
+        st_lane<NT>(GRP(st_b, 0), t, f32x4{hs[15], hs[16], hs[17], __int_as_float(step)});
+        st_lane<NT>(GRP(st_b, 1), t, f32x4{__int_as_float(epi), __int_as_float(succ), carry[3], carry[0]});
+        st_lane<NT>(GRP(st_b, 2), t, f32x4{carry[1], carry[2], ws[0], ws[1]});
+        st_lane<NT>(GRP(st_b, 3), t, f32x4{ws[2], ws[3], ws[4], hs[2]});
+        st_lane<NT>(GRP(st_b, 4), t, f32x4{hs[0], hs[1], hs[4], hs[5]});
+        st_lane<NT>(GRP(st_b, 5), t, f32x4{hs[6], hs[7], hs[8], hs[9]});
+        st_lane<NT>(GRP(st_b, 6), t, f32x4{hs[10], hs[11], hs[12], hs[13]});
+        st_lane<NT>(reinterpret_cast<f32x2*>(GRP(st_b, 7)), 2 * t, f32x2{hs[14], hs[3]});
     }
+#undef GRP
 
     TSTAMP(11, "v"(tid));
 #if HG_TIMING
@@ -1206,7 +1242,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
                            (float)e->Pd.wm[0], (float)e->Pd.wm[1], (float)e->Pd.wm[2]);
         if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "fill_wind_kernel");
     }
-    const int64_t slots = hgk::tile_words(num_envs) / hgk::kTileCols;
+    const int64_t slots = hgk::tile_words(num_envs) / hgk::kEnvSlots;
     hipLaunchKernelGGL(init_kernel, dim3(grid_for(slots)), dim3(kBlock), 0, 0, e->tmpl, e->state, slots);
     if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "init_kernel");
     if ((err = hipDeviceSynchronize()) != hipSuccess) return cleanup(err, "init sync");

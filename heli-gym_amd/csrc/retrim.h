@@ -10,19 +10,29 @@
 
 namespace hgk {
 
-// Env state in HBM: wave tiles of 64 envs, [ceil(N/64)][kTileCols][64] 32-bit words -- columns
-// 0..26 the fp32 state record (heli 18 | wind 5 | carry 4), 27..29 the int32 counters (episode
-// step, success steps, episode index).  A wave's whole state is one contiguous 7.5 KB block, so
-// every column of a step is an immediate offset from one base address.
-#ifndef HG_TILE_ENVS
-#define HG_TILE_ENVS 64
-#endif
-constexpr int kTileEnvs = HG_TILE_ENVS;
+// Env state in HBM: wave tiles of 64 envs, [ceil(N/64)][8][64][4] 32-bit words.  An env has 32
+// slots in eight groups of four; group g of a tile is 64 lanes x 16 bytes, so the step kernel moves a
+// group with one 16-byte access per lane, 1 KB contiguous per wave (8 loads and 8 stores per env
+// instead of 30 of 4 bytes).  The 30 logical columns -- the fp32 state record 0..26 (heli 18 | wind 5
+// | carry 4) and the int32 counters 27..29 (episode step, success steps, episode index) -- sit in the
+// groups in the order the step needs them: position and step counter, the noise key and carry, the
+// wind state, then the heli state; slots 30 and 31 are padding, never read or written by the step.
+constexpr int kTileEnvs = 64;
+static_assert(HG_STATE_COLS + HG_COUNTER_COLS == 30, "the slot table covers 30 columns");
 constexpr int kCtrCol0 = HG_STATE_COLS;
-constexpr int kTileCols = HG_STATE_COLS + HG_COUNTER_COLS;
-constexpr int kTileWords = kTileCols * kTileEnvs;
+constexpr int kTileCols = HG_STATE_COLS + HG_COUNTER_COLS;   // logical columns
+constexpr int kEnvSlots = 32;
+constexpr int kTileWords = kEnvSlots * kTileEnvs;
+// slot of logical column c:  x y z step | epi succ carry3 carry0 | carry1 carry2 ws0 ws1 |
+// ws2 ws3 ws4 psi_mr | vi_mr vi_tr b0 b1 | u v w p | q r phi theta | psi psi_tr - -
+__host__ __device__ constexpr int slot_of(int c) {
+    constexpr int t[30] = {16, 17, 15, 29, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 0, 1, 2,
+                           10, 11, 12, 13, 14, 7, 8, 9, 6, 3, 5, 4};
+    return t[c];
+}
 __host__ __device__ inline int64_t tix(int64_t env, int col) {
-    return (env / kTileEnvs) * kTileWords + col * kTileEnvs + (env % kTileEnvs);
+    const int s = slot_of(col);
+    return (env / kTileEnvs) * kTileWords + (s >> 2) * (4 * kTileEnvs) + (env % kTileEnvs) * 4 + (s & 3);
 }
 inline int64_t tile_words(int64_t n) { return ((n + kTileEnvs - 1) / kTileEnvs) * kTileWords; }
 

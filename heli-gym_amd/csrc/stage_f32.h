@@ -28,6 +28,10 @@
 
 #include "physics.h"
 
+#ifndef HG_STAGE_STAMP   // diagnostic phase stamps (HG_TIMING builds of heligym_amd.hip)
+#define HG_STAGE_STAMP(j, ...) do { } while (0)
+#endif
+
 namespace hg {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -55,6 +59,61 @@ struct StepCtx {
     float cz;             // the gear cannot touch while z < cz (committed-ground bound, conservative)
     Ground<float> g;      // ground under the committed x, y (F6)
 };
+
+// The model constants the stages use as packed operands, built once per step.  As instruction
+// operands a pair of constants must sit in a register pair: left to the compiler, each use
+// re-materialises it with two s_mov (which a lone wave issues as slowly as a VALU instruction), so
+// the pairs are made opaque (pin) and live in VGPRs across the four stages.
+struct StepK {
+    f2 is0;                  // (IS_MR, 0)
+    f2 coef;                 // (COEF_TH_MR, COEF_TH_TR)
+    f2 inflow_thr, inflow;   // inflow ODE coefficients (MR, TR)
+    f2 hxy;                  // (XUU / 2, YVV / 2)
+    f2 zmax, zuu, zuw;       // (HT, VT) stall / linear coefficients
+    f2 one_m1, mh_h;         // (1, -1), (-H_MR, H_MR)
+    f2 j0, j2, g_pq, g_qr;   // I^-1 columns for (p', r') and the gyroscopic coefficients
+    f2 k1, dl_db1;           // (K1, K1), (DL_DB1, DL_DB1)
+    f2 c6, c24;              // (-1/6, -1/6), (1/24, 1/24)
+};
+
+HD void pin(f2& x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    asm volatile("" : "+v"(x));
+#else
+    (void)x;
+#endif
+}
+
+// PIN: a lone wave per SIMD (the launch fits one wave per SIMD), where a scalar instruction costs the
+// wave an issue slot and registers are free; with several waves per SIMD the compiler's choice
+// (constants re-materialised by SALU, which co-issues with other waves' VALU) keeps VGPRs for occupancy.
+template <bool PIN>
+HD StepK step_k(const Params<float>& P) {
+    StepK K;
+    K.is0 = f2{P.mr_IS, 0.f};
+    K.coef = f2{P.mr_coef, P.tr_coef};
+    K.inflow_thr = f2{P.f_mr_inflow_thr, P.f_tr_inflow_thr};
+    K.inflow = f2{P.mr_inflow, P.tr_inflow};
+    K.hxy = f2{P.f_hXUU, P.f_hYVV};
+    K.zmax = f2{P.ht_ZMAX, P.vt_YMAX};
+    K.zuu = f2{P.ht_ZUU, P.vt_YUU};
+    K.zuw = f2{P.ht_ZUW, P.vt_YUV};
+    K.one_m1 = f2{1.f, -1.f};
+    K.mh_h = f2{-P.mr_H, P.mr_H};
+    K.j0 = f2{P.Ji00, P.Ji20};
+    K.j2 = f2{P.Ji02, P.Ji22};
+    K.g_pq = f2{P.f_gyro[0], P.f_gyro[1]};
+    K.g_qr = f2{P.f_gyro[2], P.f_gyro[3]};
+    K.k1 = f2{P.mr_K1, P.mr_K1};
+    K.dl_db1 = f2{P.mr_DL_DB1, P.mr_DL_DB1};
+    K.c6 = f2{-1.f / 6.f, -1.f / 6.f};
+    K.c24 = f2{1.f / 24.f, 1.f / 24.f};
+    if (!PIN) return K;
+    pin(K.is0); pin(K.coef); pin(K.inflow_thr); pin(K.inflow); pin(K.hxy); pin(K.zmax); pin(K.zuu);
+    pin(K.zuw); pin(K.one_m1); pin(K.mh_h); pin(K.j0); pin(K.j2); pin(K.g_pq); pin(K.g_qr); pin(K.k1);
+    pin(K.dl_db1); pin(K.c6); pin(K.c24);
+    return K;
+}
 
 // (sin, cos) of the three attitude angles
 struct Att2 {
@@ -108,16 +167,16 @@ HD StepCtx step_ctx(const Params<float>& P, float a0, float a1, float a2, float 
 
 // Attitude of a stage from the committed one by the angle-addition formulas (physics.h
 // attitude_step), on (sin, cos) pairs; a wave with a large stage increment takes the full sincos.
-HD Att2 att_step(const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
+HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
     const f2 d01 = pp - pp0;   // phi, psi increments
     const float d2 = th - th0;
     // sin d = d - d^3/6, cos d = 1 - d^2/2 + d^4/24 (|d| <= 0.05: within 2.7e-9 / 2.2e-11)
     const f2 q01 = d01 * d01;
-    const f2 sd01 = d01 + (d01 * q01) * (-1.f / 6.f);
-    const f2 cd01 = 1.f + q01 * (-0.5f + q01 * (1.f / 24.f));
+    const f2 sd01 = d01 + (d01 * q01) * K.c6;
+    const f2 cd01 = 1.f + q01 * (-0.5f + q01 * K.c24);
     const float q2 = d2 * d2;
-    const float sd2 = d2 + (d2 * q2) * (-1.f / 6.f);
-    const float cd2 = 1.f + q2 * (-0.5f + q2 * (1.f / 24.f));
+    const float sd2 = d2 + (d2 * q2) * K.c6.x;
+    const float cd2 = 1.f + q2 * (-0.5f + q2 * K.c24.x);
     // (sin, cos)(e + d) = (s, c) cd + (c, -s) sd
     const f2 A0 = a0.a[0], A1 = a0.a[1], A2 = a0.a[2];
     Att2 a;
@@ -143,7 +202,7 @@ HD Att2 att_step(const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
 // One evaluation of the model at stage state s (helicopter_dynamics.py:400-489) -> derivatives k;
 // with OBS also the 17 observations (:471-488) and the total power.
 template <bool OBS>
-HD void stage_f32(const Params<float>& P, const StepCtx& c, const X16& s, const Att2& at, X16& k,
+HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, const X16& s, const Att2& at, X16& k,
                   float* __restrict__ obs) {
 #ifdef HG_ISA_MARKS
     asm volatile("; HGMARK stage begin");
@@ -179,7 +238,7 @@ HD void stage_f32(const Params<float>& P, const StepCtx& c, const X16& s, const 
 
     // ---- main rotor (:203-270) and tail rotor (:272-300), packed as (MR, TR)
     const f2 B = s.b;
-    const f2 BM = B - f2{P.mr_IS, 0.f};                        // (b0 - IS, b1)
+    const f2 BM = B - K.is0;                        // (b0 - IS, b1)
     const float ua2 = ua * ua;
     const float wr = wa + BM.x * ua - BM.y * va;               // (:222-224)
     const float wq = wa + q * P.tr_D;                          // (:276-279)
@@ -189,12 +248,12 @@ HD void stage_f32(const Params<float>& P, const StepCtx& c, const X16& s, const 
     const f2 wrvr = f2{wr, vr};
     const f2 wb = wrvr + c.wb0 + vadv * c.wb1;                 // blade-relative inflow (:226, :281)
     const f2 dth = wb - s.vi;                                  // thrust = dth rho coef (:246, :284)
-    const f2 thr = dth * (rho * f2{P.mr_coef, P.tr_coef});
+    const f2 thr = dth * (rho * K.coef);
     const f2 dw = wrvr - s.vi;
     const f2 sq = dw * dw + vadv;
     const f2 sr = f2{m_sqrt(sq.x), m_sqrt(sq.y)};
     // inflow ODEs (:247-249, :285-286)
-    const f2 dvi = dth * f2{P.f_mr_inflow_thr, P.f_tr_inflow_thr} - f2{P.mr_inflow, P.tr_inflow} * (s.vi * sr);
+    const f2 dvi = dth * K.inflow_thr - K.inflow * (s.vi * sr);
     const f2 pw = thr * dw;                                    // -(induced power) of each rotor (:250, :292)
     const float power_mr = rho * P.mr_prof * (P.mr_vtip2 + 3.f * vadv.x) - pw.x;
     const float power_tr = -pw.y;
@@ -213,14 +272,14 @@ HD void stage_f32(const Params<float>& P, const StepCtx& c, const X16& s, const 
     const f2 XYn = BM * f2{thr.x, -thr.x};                     // -(X_MR, Y_MR)
     const float DL_DA1 = rho * P.mr_DL_DA1_dro;
     // (b0 + lon - K1 b1, lat - b1 - K1 b0)
-    const f2 inner = B * f2{1.f, -1.f} + c.lon_lat - P.mr_K1 * B.yx;
+    const f2 inner = B * K.one_m1 + c.lon_lat - K.k1 * B.yx;
     // (L, M) = H (Y, -X) + DL_DB1 (b1, b0) + DL_DA1 inner
-    const f2 LM_MR = XYn.yx * f2{-P.mr_H, P.mr_H} + P.mr_DL_DB1 * B.yx + DL_DA1 * inner;
+    const f2 LM_MR = XYn.yx * K.mh_h + K.dl_db1 * B.yx + DL_DA1 * inner;
 
     // ---- fuselage (:302-320)
     const float wa_f0 = wa - s.vi.x;
     const float wa_f = wa_f0 > 0.f ? wa_f0 + (float)kEps : wa_f0;
-    const f2 XY_F = (rho * f2{P.f_hXUU, P.f_hYVV}) * f2{m_fabs(ua) * ua, m_fabs(va) * va};
+    const f2 XY_F = (rho * K.hxy) * f2{m_fabs(ua) * ua, m_fabs(va) * va};
     const float awf = m_fabs(wa_f);
     const float Z_F = rho * P.f_hZWW * (awf * wa_f);
     const float zd = rho * P.f_zd * awf * (ua * P.fus_dfw_k + P.fus_dfw_c * wa_f);   // Z_F d_fw
@@ -236,8 +295,8 @@ HD void stage_f32(const Params<float>& P, const StepCtx& c, const X16& s, const 
     const f2 X = f2{wa_ht, va_vt};
     const float aua = m_fabs(ua);
     const f2 S2 = X * X + f2{vadv.x, ua2};
-    const f2 stall = f2{P.ht_ZMAX, P.vt_YMAX} * f2{m_sqrt(S2.x), m_sqrt(S2.y)} * X;
-    const f2 lin = (f2{P.ht_ZUU, P.vt_YUU} * ua + f2{P.ht_ZUW, P.vt_YUV} * X) * aua;
+    const f2 stall = K.zmax * f2{m_sqrt(S2.x), m_sqrt(S2.y)} * X;
+    const f2 lin = (K.zuu * ua + K.zuw * X) * aua;
     const float lim = 0.3f * aua;
     const f2 ZY = (0.5f * rho) * f2{m_fabs(wa_ht) > lim ? stall.x : lin.x, m_fabs(va_vt) > lim ? stall.y : lin.y};
 
@@ -303,8 +362,7 @@ HD void stage_f32(const Params<float>& P, const StepCtx& c, const X16& s, const 
     const float pq_ = p * q;
     const f2 qrpr = s.pq.yx * r;                               // (q r, p r)
     const float rrpp = r * r - p * p;
-    const f2 dpr = f2{P.Ji00, P.Ji20} * Mx + f2{P.Ji02, P.Ji22} * Mz + f2{P.f_gyro[0], P.f_gyro[1]} * pq_ +
-                   f2{P.f_gyro[2], P.f_gyro[3]} * qrpr.x;
+    const f2 dpr = K.j0 * Mx + K.j2 * Mz + K.g_pq * pq_ + K.g_qr * qrpr.x;
     const float dq = P.Ji11 * My + P.f_gyro[4] * qrpr.y + P.f_gyro[5] * rrpp;
     k.vi = dvi;
     k.b = dB;
@@ -367,6 +425,7 @@ HD void from_x16(const X16& x, float* s) {   // (s[2], s[3], the rotor azimuths,
 
 // One RK4 step of the 18-state model (dynamics.py:158-171): hs advanced in place, k4 (the
 // reference's state_dots, what the reward reads) in d, the stage-4 observation in obs.
+template <bool LONE>
 HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,
                      float* __restrict__ obs) {
     X16 h = to_x16(hs);
@@ -375,13 +434,20 @@ HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict
     a0.a[1] = sincos2(h.rt.y);
     a0.a[2] = sincos2(h.pp.y);
     X16 k, acc, st;
-    stage_f32<false>(P, c, h, a0, k, obs);
+#ifndef HG_PIN_CONSTANTS
+#define HG_PIN_CONSTANTS 1
+#endif
+    const StepK K = step_k<LONE && HG_PIN_CONSTANTS>(P);
+    stage_f32<false>(P, K, c, h, a0, k, obs);
+    HG_STAGE_STAMP(5, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<true>(h, k, acc, st, P.half_dt);
-    stage_f32<false>(P, c, st, att_step(a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<false>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    HG_STAGE_STAMP(6, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<false>(h, k, acc, st, P.half_dt);
-    stage_f32<false>(P, c, st, att_step(a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<false>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    HG_STAGE_STAMP(7, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<false>(h, k, acc, st, P.dt);
-    stage_f32<true>(P, c, st, att_step(a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<true>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     rk_update2(h, k, acc, P.dt6);
     from_x16(h, hs);
     // rotor azimuths: constant rates (:457-458), dt / 6 (O + 2 O + 2 O + O) = dt O

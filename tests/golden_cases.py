@@ -114,11 +114,13 @@ def _terminal_bounds(arg, arg_tol, d):
 
 
 def reward_bounds(heli, dots, task, n_t=np.sqrt(2 * 18 / 32.2), n_x=36.0, n_v=np.sqrt(2 * 18 * 32.2),
-                  n_a=32.2, sea_alt=4000.0, vel=100.0):
+                  n_a=32.2, sea_alt=4000.0, vel=100.0, tol=None):
     """Interval of task rewards (helicopter_with_tasks.py:27-52, 78-115) consistent with the
     post-step state `heli` and k4 derivatives `dots` once every sign() argument that lies within
     the parity tolerance of zero is treated as ambiguous: the reward jumps there.  Also returns
-    the magnitude scale of the reward's terms (sum of |term|), the scale rounding errors follow."""
+    the magnitude scale of the reward's terms (sum of |term|), the scale rounding errors follow.
+    tol: the state tolerance x -> |dx| deciding the ambiguity (default contract (i))."""
+    _tol = tol or globals()["_tol"]
     h = np.asarray(heli, dtype=np.float64)
     d = np.asarray(dots, dtype=np.float64)
     pn, pdn = h[:, 9:12] * n_t, d[:, 9:12] * n_t ** 2

@@ -456,10 +456,17 @@ def test_ragged_batch_sizes(torch, n):
     o = obs.cpu().numpy().astype(np.float64)
     done = (term | trunc).cpu().numpy()
     tmpl = env.template()["obs"]
+    # each step's own measured rounding terms (input rounding + KAPPA_ULP altitude ulps, ~0 off the
+    # ground; tests/rounding_terms.py), as in check_vs_reference: no blanket factor for contact steps
+    import rounding_terms
+    r_obs, _, _ = rounding_terms.load("0.01/hover")
+    u_obs, _, _ = rounding_terms.load_ulp("0.01/hover")
+    r_obs = r_obs + KAPPA_ULP * u_obs
+    assert len(r_obs) == len(b["obs"])
     for j in range(n):
         ref = tmpl if done[j] else b["obs"][idx[j]]
-        tol = 1e-6 if done[j] else STEP_ABS + STEP_REL * np.abs(ref)
-        assert np.all(gc.step_errors(o[j], ref, gc.OBS_ANGLE_COLS) <= tol + 4 * (b["obs"][idx[j], 16] < 10) * tol), j
+        tol = 1e-6 if done[j] else STEP_ABS + STEP_REL * np.abs(ref) + r_obs[idx[j]]
+        assert np.all(gc.step_errors(o[j], ref, gc.OBS_ANGLE_COLS) <= tol), j
     np.testing.assert_array_equal(np.sort(info["reset_index"].cpu().numpy()), np.nonzero(done)[0])
     env.close()
 
@@ -1059,7 +1066,7 @@ def test_full_size_trajectories_vs_oracle(torch, terrain_u16, task, N):
     acts = torch.rand((T, N, 4), generator=g, device=env.device) * 2 - 1
     etas = torch.randn((T, N, 3), generator=g, device=env.device) / np.sqrt(dt)
     ti = torch.as_tensor(idx, device=env.device)
-    obs_k, rew_k = [], []
+    obs_k, rew_k = [], []   # (reward checked at every pre-contact step of the sampled envs, below)
     nonfinite_obs, nan_rew_bad = 0, 0
     for t in range(T):
         env.step_async(acts[t], eta=etas[t], with_reset_info=False)
@@ -1087,7 +1094,8 @@ def test_full_size_trajectories_vs_oracle(torch, terrain_u16, task, N):
     env.close()
     cfg, _ = config.make_config(task=task, dt=dt, target={"vel": 100.0, "heading": 0.0})
     orc = Oracle(cfg, terrain_u16)
-    worst, compared = 0.0, 0
+    worst, compared, worst_rew = 0.0, 0, 0.0
+    traj_tol = lambda x: TRAJ_ABS + TRAJ_REL * np.abs(x)   # noqa: E731  contract (ii) on the state
     for j, i in enumerate(idx):
         s = s0[i]
         prev_obs = np.zeros(17)
@@ -1113,8 +1121,15 @@ def test_full_size_trajectories_vs_oracle(torch, terrain_u16, task, N):
             assert np.all(err <= tol), (int(i), t, err)
             worst = max(worst, float((err / tol).max()))
             compared += 1
+            if t > 0:   # the task reward at every pre-contact step: contract (ii) scaled like the state
+                lo, hi, scale = gc.reward_bounds(np.array(e.heli)[None], np.array(e.dots)[None], task, tol=traj_tol)
+                rt = (REWARD_ABS + REWARD_REL * scale[0]) * (TRAJ_ABS / STEP_ABS)
+                r = rew_k[t, j]
+                assert lo[0] - rt <= r <= hi[0] + rt, (int(i), t, r, lo[0], hi[0], rt)
+                worst_rew = max(worst_rew, float(max(lo[0] - r, r - hi[0], 0.0) / rt))
     assert compared > S * T // 4
-    print(f"\n[full-size {task} x {N}] {compared} env-steps compared, worst error / tolerance {worst:.3f}")
+    print(f"\n[full-size {task} x {N}] {compared} env-steps compared, worst error / tolerance {worst:.3f}, "
+          f"reward outside its interval / tolerance {worst_rew:.3f}")
 
 
 def test_single_env_dropin_equals_vector_env(torch):
