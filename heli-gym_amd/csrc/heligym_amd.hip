@@ -68,12 +68,9 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
-#ifndef HG_PHILOX_ROUNDS
-#define HG_PHILOX_ROUNDS 10
-#endif
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int i = 0; i < HG_PHILOX_ROUNDS; ++i) {
+    for (int i = 0; i < 10; ++i) {
         const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
         const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
         c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
@@ -149,21 +146,10 @@ __device__ __forceinline__ void st_out(T* p, T v) {
     if constexpr (NT && sizeof(T) >= 4) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
-#ifndef HG_WT   // experiment: write-through (sc1) output stores, as pairs of 8-byte agent-scope stores
-#define HG_WT 0
-#endif
-__device__ __forceinline__ void st_wt8(void* p, uint64_t v) {
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 template <bool NT>
 __device__ __forceinline__ void st_out4(float* p, const float* s) {
     const f32x4 v = *reinterpret_cast<const f32x4*>(s);
-    if constexpr (HG_WT && NT) {
-        const uint64_t lo = __builtin_bit_cast(uint64_t, __builtin_shufflevector(v, v, 0, 1));
-        const uint64_t hi = __builtin_bit_cast(uint64_t, __builtin_shufflevector(v, v, 2, 3));
-        st_wt8(p, lo);
-        st_wt8(p + 2, hi);
-    } else if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(p));
     else *reinterpret_cast<f32x4*>(p) = v;
 }
 
@@ -192,14 +178,7 @@ __device__ __forceinline__ T ld_lane(const T* __restrict__ base, uint32_t idx) {
 template <bool NT, typename T>
 __device__ __forceinline__ void st_lane(T* base, uint32_t idx, T v) {
     HG_GLOBAL T* p = (HG_GLOBAL T*)((HG_GLOBAL char*)base + idx * (uint32_t)sizeof(T));
-    if constexpr (HG_WT && NT && sizeof(T) == 16) {
-        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-        const u64x2 w = __builtin_bit_cast(u64x2, v);
-        __hip_atomic_store((HG_GLOBAL uint64_t*)p, (uint64_t)w.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store((HG_GLOBAL uint64_t*)p + 1, (uint64_t)w.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if constexpr (HG_WT && NT && sizeof(T) == 8) {
-        __hip_atomic_store((HG_GLOBAL uint64_t*)p, __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if constexpr (NT && sizeof(T) >= 4) __builtin_nontemporal_store(v, p);
+    if constexpr (NT && sizeof(T) >= 4) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
@@ -284,13 +263,16 @@ __device__ __forceinline__ void draw_eta(const StepArgs& a, uint64_t seed, int64
         const uint64_t gid = (uint64_t)(env_offset + blk0 + lo);
         const U4 r = philox(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)epi},
                             (uint32_t)seed, (uint32_t)(seed >> 32));
-        float sn, cs;
-        const float r0 = sqrtf(-2.f * __logf(u01(r.x)));
-        __sincosf(6.28318530717958648f * u01(r.y), &sn, &cs);
-        const float r1 = sqrtf(-2.f * __logf(u01(r.z)));
-        eta[0] = r0 * cs * P.eta_norm;
-        eta[1] = r0 * sn * P.eta_norm;
-        eta[2] = r1 * __cosf(6.28318530717958648f * u01(r.w)) * P.eta_norm;
+        // Box-Muller.  Radii sqrt(-2 ln u) / sqrt(dt) = sqrt(log2(u) * (-2 ln 2 / dt)) with u in (0, 1)
+        // from the top 24 bits; angles in revolutions for the hardware sin / cos (v_sin_f32 takes
+        // revolutions: sin(2 pi u) = v_sin(u)), u in [1, 2) from the top 23 bits (a whole turn apart)
+        const float rk = P.eta_norm * P.eta_norm * -1.38629436111989061f;   // -2 ln 2 / dt
+        const float r0 = sqrtf(__log2f(u01(r.x)) * rk);
+        const float r1 = sqrtf(__log2f(u01(r.z)) * rk);
+        const float a1 = __uint_as_float((r.y >> 9) | 0x3f800000u), a3 = __uint_as_float((r.w >> 9) | 0x3f800000u);
+        eta[0] = r0 * __builtin_amdgcn_cosf(a1);
+        eta[1] = r0 * __builtin_amdgcn_sinf(a1);
+        eta[2] = r1 * __builtin_amdgcn_cosf(a3);
     }
 }
 
@@ -412,7 +394,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     // ground height under the committed position (F6), wind step (Heli.step :195-199)
     TSTAMP(2, "v"(eta[2]), "v"(eta[0]));
     float W[3];
-    hg::wind_step(P, ws, carry, eta, W);
+    hg::wind_step_f32(P, ws, carry, eta, W);
     TSTAMP(3, "v"(W[2]), "v"(W[0]));
     const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
 

@@ -115,6 +115,45 @@ HD StepK step_k(const Params<float>& P) {
     return K;
 }
 
+// WindDynamics.step (dynamics.py:158-171 + wind_dynamics.py:85-125) for the fp32 step, the v and
+// w filters (the same second-order form with their own time constant) packed as pairs
+// Q = (vs0, ws0), R = (vs1, ws1); u is the first-order filter.  QUIRK: the update is
+// s += dt k4, the stage inputs still formed from k1..k3; the wind output from the stage-4 input.
+// Same operations per component as physics.h wind_step, so the same roundings.
+HD void wind_step_f32(const Params<float>& P, float s[5], const float carry[4], const float eta[3], float W[3]) {
+    const WindPar<float> w = wind_params(P, carry);
+    const f2 A = f2{w.a_v, w.a_w}, B = f2{w.b_v, w.b_w}, E = f2{eta[1], eta[2]};
+    const float U = s[0];
+    const f2 Q = f2{s[1], s[3]}, R = f2{s[2], s[4]};
+    const float h = P.half_dt, dt = P.dt;
+    // stage 1..3 inputs: (U, Q, R) + h (kU, kQ, kR), kR = Q
+    float kU = w.a_u * (eta[0] - U);
+    f2 kQ = B * (E - R) - A * Q;
+    float U1 = U + kU * h;
+    f2 Q1 = Q + kQ * h, R1 = R + Q * h;
+    kU = w.a_u * (eta[0] - U1);
+    kQ = B * (E - R1) - A * Q1;
+    float U2 = U + kU * h;
+    f2 Q2 = Q + kQ * h, R2 = R + Q1 * h;
+    kU = w.a_u * (eta[0] - U2);
+    kQ = B * (E - R2) - A * Q2;
+    const float U3 = U + kU * dt;
+    const f2 Q3 = Q + kQ * dt, R3 = R + Q2 * dt;
+    kU = w.a_u * (eta[0] - U3);
+    kQ = B * (E - R3) - A * Q3;
+    // output at the stage-4 input (wind_dynamics.py:111-123)
+    const float ut = w.K_u * U3;
+    const f2 vw = f2{w.K_v, w.K_w} * (R3 + (float)(2 * kSqrt3) * Q3);
+    W[0] = P.wm[0] + (w.cos_az * ut - w.sin_az * vw.x);
+    W[1] = P.wm[1] + (w.sin_az * ut + w.cos_az * vw.x);
+    W[2] = P.wm[2] + vw.y;
+    // update with k4 only (F3)
+    s[0] = U + dt * kU;
+    const f2 Qn = Q + dt * kQ, Rn = R + dt * Q3;
+    s[1] = Qn.x; s[3] = Qn.y;
+    s[2] = Rn.x; s[4] = Rn.y;
+}
+
 // (sin, cos) of the three attitude angles
 struct Att2 {
     f2 a[3];

@@ -22,9 +22,13 @@ __global__ void probe_new(const float* __restrict__ in, float* __restrict__ out,
     a.a[0] = f2{q[40], q[41]}; a.a[1] = f2{q[42], q[43]}; a.a[2] = f2{q[44], q[45]};
     X16 k;
 #ifdef PROBE_ATT
-    a = att_step(a, f2{q[46], q[47]}, q[48], s.pp, s.rt.y);
+    const StepK K = step_k<true>(P);
+    a = att_step(K, a, f2{q[46], q[47]}, q[48], s.pp, s.rt.y);
 #endif
-    stage_f32<false>(P, c, s, a, k, nullptr);
+#ifndef PROBE_ATT
+    const StepK K = step_k<true>(P);
+#endif
+    stage_f32<false>(P, K, c, s, a, k, nullptr);
     float* o = out + i * 18;
     from_x16(k, o);
     asm volatile("; PROBE end" ::: "memory");
