@@ -18,6 +18,7 @@
 #include <string.h>
 
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/heligym_amd.h"
@@ -1050,9 +1051,37 @@ static inline unsigned retrim_grid(int64_t jobs) {
 #define STEP_KARGS(e) (e)->state, (int64_t)(e)->n, (uint64_t)(e)->cfg.seed, (int64_t)(e)->cfg.env_offset, PARAM_ARG(e), \
                       (e)->tmpl_dev
 
-// The default airframe's constant-specialised step (baked.h), with or without the optional features.
-#define HG_LAUNCH_SPECIALISED(T, ETA_, NT_, FEAT_, MULTI_)                                                 \
-    hipLaunchKernelGGL((step_kernel<T, ETA_, NT_, FEAT_, MULTI_, true>), grid, block, 0, s, STEP_KARGS(e), a)
+template <int T, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
+static void launch_step(const hg_env* e, hipStream_t s, const StepArgs& a) {
+    const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock);
+    hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED>), dim3(grid), dim3(kStepBlock), 0, s, STEP_KARGS(e), a);
+}
+
+// The step variant for a launch: NT when the batch fits one wave per SIMD; the default airframe's
+// constant-specialised kernel (baked.h) when the env uses it; with or without the optional features.
+template <int T, bool MULTI>
+static void dispatch_step(const hg_env* e, hipStream_t s, const StepArgs& a, bool eta, bool feat) {
+    auto pick = [&](auto nt) {
+        constexpr bool NT = decltype(nt)::value;
+        if (e->baked) {
+            if (feat) eta ? launch_step<T, true, NT, true, MULTI, true>(e, s, a) : launch_step<T, false, NT, true, MULTI, true>(e, s, a);
+            else eta ? launch_step<T, true, NT, false, MULTI, true>(e, s, a) : launch_step<T, false, NT, false, MULTI, true>(e, s, a);
+        } else {
+            if (feat) eta ? launch_step<T, true, NT, true, MULTI, false>(e, s, a) : launch_step<T, false, NT, true, MULTI, false>(e, s, a);
+            else eta ? launch_step<T, true, NT, false, MULTI, false>(e, s, a) : launch_step<T, false, NT, false, MULTI, false>(e, s, a);
+        }
+    };
+    if (e->n <= e->resident_envs) pick(std::true_type{});
+    else pick(std::false_type{});
+}
+template <bool MULTI>
+static void dispatch_task(const hg_env* e, hipStream_t s, const StepArgs& a, bool eta, bool feat) {
+    switch (e->cfg.task) {
+        case HG_TASK_HOVER: dispatch_step<HG_TASK_HOVER, MULTI>(e, s, a, eta, feat); break;
+        case HG_TASK_FORWARD_FLIGHT: dispatch_step<HG_TASK_FORWARD_FLIGHT, MULTI>(e, s, a, eta, feat); break;
+        default: dispatch_step<HG_TASK_HELI, MULTI>(e, s, a, eta, feat); break;
+    }
+}
 
 extern "C" {
 #if HG_TIMING
@@ -1385,38 +1414,9 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.retrim_slot = rt_slot;
     a.tmpl_env = e->tmpl_env;
     a.nsteps = 1;
-    const dim3 grid((unsigned)((e->n + kStepBlock - 1) / kStepBlock)), block(kStepBlock);
     const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next ||
                       e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
-#define HG_LAUNCH_STEP_NT(T, NT)                                                                                 \
-    do {                                                                                                         \
-        if (e->baked) {                                                                                          \
-            if (feat) {                                                                                          \
-                if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, true, false);                                        \
-                else HG_LAUNCH_SPECIALISED(T, false, NT, true, false);                                           \
-            } else {                                                                                             \
-                if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, false, false);                                       \
-                else HG_LAUNCH_SPECIALISED(T, false, NT, false, false);                                          \
-            }                                                                                                    \
-        } else if (feat) {                                                                                       \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, false, false>), grid, block, 0, s, STEP_KARGS(e), a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, false, false>), grid, block, 0, s, STEP_KARGS(e), a);    \
-        } else {                                                                                                 \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, false, false>), grid, block, 0, s, STEP_KARGS(e), a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, false, false>), grid, block, 0, s, STEP_KARGS(e), a);    \
-        }                                                                                                        \
-    } while (0)
-#define HG_LAUNCH_STEP(T)                                   \
-    do {                                                    \
-        if (e->n <= e->resident_envs) HG_LAUNCH_STEP_NT(T, true); \
-        else HG_LAUNCH_STEP_NT(T, false);                   \
-    } while (0)
-    switch (e->cfg.task) {
-        case HG_TASK_HOVER: HG_LAUNCH_STEP(HG_TASK_HOVER); break;
-        case HG_TASK_FORWARD_FLIGHT: HG_LAUNCH_STEP(HG_TASK_FORWARD_FLIGHT); break;
-        default: HG_LAUNCH_STEP(HG_TASK_HELI); break;
-    }
-#undef HG_LAUNCH_STEP_NT
+    dispatch_task<false>(e, s, a, eta != nullptr, feat);
     HIP_TRY(hipGetLastError());
     if (retrim) {   // re-trim this step's resets against their last wind (overwrites the template)
         hgk::RetrimArgs r;
@@ -1432,7 +1432,6 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.fail_count = e->retrim_count + 1;
         HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), s));
     }
-#undef HG_LAUNCH_STEP
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }
@@ -1485,38 +1484,8 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     a.nsteps = nsteps;
     a.retrim_slot = -1;
     hipStream_t s = (hipStream_t)stream;
-    const dim3 grid((unsigned)((e->n + kStepBlock - 1) / kStepBlock)), block(kStepBlock);
     const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
-#define HG_LAUNCH_ROLL_NT(T, NT)                                                                                 \
-    do {                                                                                                         \
-        if (e->baked) {                                                                                          \
-            if (feat) {                                                                                          \
-                if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, true, true);                                         \
-                else HG_LAUNCH_SPECIALISED(T, false, NT, true, true);                                            \
-            } else {                                                                                             \
-                if (eta) HG_LAUNCH_SPECIALISED(T, true, NT, false, true);                                        \
-                else HG_LAUNCH_SPECIALISED(T, false, NT, false, true);                                           \
-            }                                                                                                    \
-        } else if (feat) {                                                                                       \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, true, true, false>), grid, block, 0, s, STEP_KARGS(e), a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, true, true, false>), grid, block, 0, s, STEP_KARGS(e), a);    \
-        } else {                                                                                                 \
-            if (eta) hipLaunchKernelGGL((step_kernel<T, true, NT, false, true, false>), grid, block, 0, s, STEP_KARGS(e), a); \
-            else hipLaunchKernelGGL((step_kernel<T, false, NT, false, true, false>), grid, block, 0, s, STEP_KARGS(e), a);    \
-        }                                                                                                        \
-    } while (0)
-#define HG_LAUNCH_ROLL(T)                                   \
-    do {                                                    \
-        if (e->n <= e->resident_envs) HG_LAUNCH_ROLL_NT(T, true); \
-        else HG_LAUNCH_ROLL_NT(T, false);                   \
-    } while (0)
-    switch (e->cfg.task) {
-        case HG_TASK_HOVER: HG_LAUNCH_ROLL(HG_TASK_HOVER); break;
-        case HG_TASK_FORWARD_FLIGHT: HG_LAUNCH_ROLL(HG_TASK_FORWARD_FLIGHT); break;
-        default: HG_LAUNCH_ROLL(HG_TASK_HELI); break;
-    }
-#undef HG_LAUNCH_ROLL
-#undef HG_LAUNCH_ROLL_NT
+    dispatch_task<true>(e, s, a, eta != nullptr, feat);
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }

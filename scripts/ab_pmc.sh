@@ -3,7 +3,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 N=${N:-65536}
-for r in 1 2 3; do
+for r in ${RS:-1 2 3}; do
   for v in cur ${B:-r02}; do
     if [ $v = cur ]; then lib=$PWD/heli-gym_amd/heligym_amd/libheligym_amd.so; else lib=$PWD/build/variants/$v.so; fi
     HELIGYM_AMD_LIB=$lib timeout -k 10 120 python bench.py --envs $N --steps 1000 --repeats 3 --no-secondary --no-cpu-baseline --no-parity > gpurun_out/ab.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/ab.log; exit 3; }

@@ -2,7 +2,7 @@
 # between the in-tree library and variants.  Each GPU step has its own limit.
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-if [ -x build/dep ]; then timeout -k 10 60 ./build/dep | tee gpurun_out/dep.txt || exit 3; fi
+if [ "${DEP:-1}" = 1 ] && [ -x build/dep ]; then timeout -k 10 60 ./build/dep | tee gpurun_out/dep.txt || exit 3; fi
 for N in ${NS:-65536 4194304}; do
   for r in 1 2; do
     for v in cur ${VARIANTS:-r02}; do
