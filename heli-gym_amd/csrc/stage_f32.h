@@ -76,6 +76,64 @@ struct StepK {
     f2 c6, c24;              // (-1/6, -1/6), (1/24, 1/24)
 };
 
+// Packed products whose sign flip or lane swap is an operand modifier of v_pk_fma_f32 (op_sel /
+// op_sel_hi pick each lane's half of a register pair, neg_lo / neg_hi negate a lane): the compiler
+// folds a broadcast-and-negate of a scalar in its own register, but not of one lane of a pair,
+// where it builds the operand with a v_xor and a v_mov first.  Written out here for the pair-lane
+// cases; the host pass (never executed) gets the plain expression.
+#ifndef HG_PK_ASM
+#define HG_PK_ASM 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && HG_PK_ASM
+#define HG_PKFMA(A, B, C, MODS, ...)                                                              \
+    ({                                                                                          \
+        f2 r_;                                                                                  \
+        asm("v_pk_fma_f32 %0, %1, %2, %3 " MODS : "=v"(r_) : "v"(A), "v"(B), "v"(C));          \
+        r_;                                                                                     \
+    })
+#define HG_PKMUL(A, B, MODS, ...)                                                                 \
+    ({                                                                                          \
+        f2 r_;                                                                                  \
+        asm("v_pk_mul_f32 %0, %1, %2 " MODS : "=v"(r_) : "v"(A), "v"(B));                      \
+        r_;                                                                                     \
+    })
+#else
+#define HG_PKFMA(A, B, C, MODS, ...) (__VA_ARGS__)
+#define HG_PKMUL(A, B, MODS, ...) (__VA_ARGS__)
+#endif
+// a.yx * (b.x, -b.x) + c
+HD f2 fma_sw_bxn(f2 a, f2 b, f2 c) {
+    return HG_PKFMA(a, b, c, "op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[0,1,0]", a.yx * f2{b.x, -b.x} + c);
+}
+// a.yx * (b.y, -b.y) + c
+HD f2 fma_sw_byn(f2 a, f2 b, f2 c) {
+    return HG_PKFMA(a, b, c, "op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]", a.yx * f2{b.y, -b.y} + c);
+}
+// a * (-b.x, b.x) + c
+HD f2 fma_nbx(f2 a, f2 b, f2 c) {
+    return HG_PKFMA(a, b, c, "op_sel_hi:[1,0,1] neg_lo:[0,1,0]", a * f2{-b.x, b.x} + c);
+}
+// a * (b.x, -b.x) - c
+HD f2 fms_bxn(f2 a, f2 b, f2 c) {
+    return HG_PKFMA(a, b, c, "op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,1,1]", a * f2{b.x, -b.x} - c);
+}
+// a * (b.x, -b.x)
+HD f2 mul_bxn(f2 a, f2 b) {
+    return HG_PKMUL(a, b, "op_sel_hi:[1,0] neg_hi:[0,1]", a * f2{b.x, -b.x});
+}
+// (a.y, -a.x) * b.x + c
+HD f2 fma_swn_bx(f2 a, f2 b, f2 c) {
+    return HG_PKFMA(a, b, c, "op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_hi:[1,0,0]", f2{a.y, -a.x} * b.x + c);
+}
+// (a.y, -a.x) * b.y + c
+HD f2 fma_swn_by(f2 a, f2 b, f2 c) {
+    return HG_PKFMA(a, b, c, "op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]", f2{a.y, -a.x} * b.y + c);
+}
+// (-a.y, a.x) * b.x + c
+HD f2 fma_nsw_bx(f2 a, f2 b, f2 c) {
+    return HG_PKFMA(a, b, c, "op_sel:[1,0,0] op_sel_hi:[0,0,1] neg_lo:[1,0,0]", f2{-a.y, a.x} * b.x + c);
+}
+
 HD void pin(f2& x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     asm volatile("" : "+v"(x));
@@ -219,9 +277,9 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
     // (sin, cos)(e + d) = (s, c) cd + (c, -s) sd
     const f2 A0 = a0.a[0], A1 = a0.a[1], A2 = a0.a[2];
     Att2 a;
-    a.a[0] = A0 * cd01.x + f2{A0.y, -A0.x} * sd01.x;
+    a.a[0] = fma_swn_bx(A0, sd01, A0 * cd01.x);
     a.a[1] = A1 * cd2 + f2{A1.y, -A1.x} * sd2;
-    a.a[2] = A2 * cd01.y + f2{A2.y, -A2.x} * sd01.y;
+    a.a[2] = fma_swn_by(A2, sd01, A2 * cd01.y);
     // a lane with a larger increment (a tumbling env) takes the full sincos, in a wave-uniform branch
     const bool small = m_fabs(d01.x) <= 0.05f && m_fabs(d01.y) <= 0.05f && m_fabs(d2) <= 0.05f;
 #ifndef HG_ISA_HOT   // (analysis builds only: the hot path without its cold branches)
@@ -253,17 +311,17 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
     // ---- kinematics (kinematic.py:3-29, :423-431).  Rotations are written so that every sign
     // flip and lane swap is an operand modifier of the packed instruction: (s, c).yx * (x, -x) etc.
     const float ic1 = m_rcp(c1);
-    const f2 sqth = SC0 * q + SC0.yx * f2{r, -r};              // (s0 q + c0 r, theta')
+    const f2 sqth = fma_sw_bxn(SC0, s.rt, SC0 * q);           // SC0 q + SC0.yx (r, -r) = (s0 q + c0 r, theta')
     const float phid = p + (s1 * ic1) * sqth.x, psid = ic1 * sqth.x;
     // NED velocity B^T uvw = Rz^T Ry^T Rx^T uvw
-    const f2 yz1 = SC0.yx * v + SC0 * f2{-w, w};                 // Rx^T (y, z)
-    const f2 xz2 = SC1.yx * f2{u, -u} + SC1 * yz1.y;           // Ry^T (x, z)
-    const f2 n01 = SC2.yx * xz2.x - SC2 * f2{yz1.x, -yz1.x};   // Rz^T (x, y)
+    const f2 yz1 = fma_nbx(SC0, s.wz, SC0.yx * v);              // SC0.yx v + SC0 (-w, w) = Rx^T (y, z)
+    const f2 xz2 = fma_sw_bxn(SC1, s.uv, SC1 * yz1.y);         // SC1.yx (u, -u) + SC1 yz1.y = Ry^T (x, z)
+    const f2 n01 = fma_nbx(SC2, yz1, SC2.yx * xz2.x);          // SC2.yx xz2.x - SC2 (y, -y) = Rz^T (x, y)
     const float n2 = xz2.y;
     // air-relative body velocity uvw - B W, B = Rx Ry Rz
     const f2 ab = SC2.yx * f2{c.W0, -c.W0} + SC2 * c.W1;       // Rz W (x, y)
     const f2 xg = SC1.yx * ab.x + SC1 * f2{-c.W2, c.W2};       // Ry (x, z)
-    const f2 yzw = SC0 * xg.y + SC0.yx * f2{ab.y, -ab.y};      // Rx (y, z)
+    const f2 yzw = fma_sw_byn(SC0, ab, SC0 * xg.y);            // SC0 xg.y + SC0.yx (ab.y, -ab.y) = Rx (y, z)
     const float ua = u - xg.x;
     const f2 vwa = f2{v, w} - yzw;
     const float va = vwa.x, wa = vwa.y;
@@ -306,9 +364,9 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
     // (a_sum, b_sum) = (b1 - lat + KC b0 + DB1DV va f1, b0 + lon - KC b1 - DB1DV ua f3)
     const f2 absum = (B.yx + c.mlat_lon) + B * f2{KC, -KC} + DB1DV * f2{va * f1, ua * f3n};
     // (b0', b1') = (-ITB2_OM a_sum - ITB b_sum - q, ITB2_OM b_sum - ITB a_sum - p)
-    const f2 dB = absum * f2{itb.x, -itb.x} - (absum.yx * itb.y + s.pq.yx);
+    const f2 dB = fms_bxn(absum, itb, absum.yx * itb.y + s.pq.yx);
     // forces and moments of the main rotor (:264-269): (X, Y) = -T (b0 - IS, -b1), Z = -T
-    const f2 XYn = BM * f2{thr.x, -thr.x};                     // -(X_MR, Y_MR)
+    const f2 XYn = mul_bxn(BM, thr);                           // BM (T, -T) = -(X_MR, Y_MR)
     const float DL_DA1 = rho * P.mr_DL_DA1_dro;
     // (b0 + lon - K1 b1, lat - b1 - K1 b0)
     const f2 inner = B * K.one_m1 + c.lon_lat - K.k1 * B.yx;
@@ -392,7 +450,8 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
 
     // ---- equations of motion (:448-470)
     // uvw' = F / m - pqr x uvw
-    const f2 duv = f2{Fx, Fyz.x} * P.inv_mass + r * f2{v, -u} + w * f2{-q, p};
+    // F / m + r (v, -u) + w (-q, p)
+    const f2 duv = fma_nsw_bx(s.pq, s.wz, fma_swn_bx(s.uv, s.rt, f2{Fx, Fyz.x} * P.inv_mass));
     const float dw_ = Fyz.y * P.inv_mass + (q * u - p * v);
     // pqr' = I^-1 (M - pqr x I pqr), I = [[Ixx,0,Ixz],[0,Iyy,0],[Ixz,0,Izz]]: the gyroscopic term is
     // (Ixz pq + (Izz-Iyy) qr, (Ixx-Izz) pr + Ixz (r^2 - p^2), (Iyy-Ixx) pq - Ixz qr) and I^-1 couples
