@@ -380,11 +380,76 @@ def gather_loop(torch, dist, env, bank, B, K, rank, world, dev, backend, overlap
     return body
 
 
+def gather_graphs(torch, dist, env, bank, B, K, rank, world, dev):
+    """The gather loop captured in hipGraphs (RCCL collectives captured with the steps): each graph
+    holds G steps, the observations alternating between two buffers; step k's gather runs on a side
+    stream concurrent with step k+1, and step k+2 waits (event) for gather k before it overwrites that
+    buffer.  A graph's side stream joins the main stream at its end, so the last gather of a graph
+    is not overlapped.  Returns (replay of exactly K steps, what the graphs keep alive)."""
+    n = env.num_envs
+    bufs = [torch.empty((n, 17), dtype=torch.float32, device=dev) for _ in range(2)]
+    gls = [[torch.empty((n, 17), dtype=torch.float32, device=dev) for _ in range(world)] if rank == 0 else None
+           for _ in range(2)]
+    G = max(2, min(B, K))
+    cap = torch.cuda.Stream(device=dev)
+    side = torch.cuda.Stream(device=dev)
+
+    def steps(count):
+        main = torch.cuda.current_stream(dev)
+        done = [None, None]
+        for k in range(count):
+            b = k & 1
+            if done[b] is not None:
+                main.wait_event(done[b])
+            env.step_async(bank[k % B], with_reset_info=False, obs_out=bufs[b])
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                dist.gather(bufs[b], gather_list=gls[b], dst=0)
+                done[b] = torch.cuda.Event()
+                done[b].record(side)
+        main.wait_stream(side)
+
+    cap.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(cap):   # warm-up outside capture (communicator, streams)
+        steps(min(G, K))
+    torch.cuda.current_stream(dev).wait_stream(cap)
+    torch.cuda.synchronize()
+    full = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(full, stream=cap):
+        steps(G)
+    rest = None
+    if K % G:
+        rest = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(rest, stream=cap):
+            steps(K % G)
+
+    def replay():
+        for _ in range(K // G):
+            full.replay()
+        if rest is not None:
+            rest.replay()
+    replay()
+    torch.cuda.synchronize()
+    return replay, (full, rest, bufs, gls, cap, side), G
+
+
 def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev, backend):
-    """BASELINE config 5 on this rank's shard: the gather loop and the plain (graph) steps."""
+    """BASELINE config 5 on this rank's shard: the gather loop (hipGraphs of steps + RCCL gathers, or
+    eager where capture is unavailable) and the plain (graph) steps."""
     K5 = min(K, 500)
-    body = gather_loop(torch, dist, env5, bank5, B, K5, rank, world, dev, backend)
-    body(min(args.warmup, K5))
+    mode5, body = None, None
+    if backend == "nccl" and not args.dry_run and os.environ.get("HG_BENCH_CONFIG5_EAGER") != "1":
+        try:
+            body, _keep5, G5 = gather_graphs(torch, dist, env5, bank5, B, K5, rank, world, dev)
+            mode5 = (f"hipGraph: graphs of {G5} steps, each step's dist.gather of obs to rank 0 captured with it "
+                     "(side stream, double-buffered)")
+        except Exception as exc:   # capture unsupported here: measure the eager loop instead, and say so
+            torch.cuda.synchronize()
+            body, mode5 = None, f"eager (graph capture of the gather failed: {type(exc).__name__}: {exc})"
+    if body is None:
+        body = gather_loop(torch, dist, env5, bank5, B, K5, rank, world, dev, backend)
+        body(min(args.warmup, K5))
+        mode5 = mode5 or "eager, dist.gather of obs to rank 0 every step, double-buffered"
     s_g5, _, _ = timer.run(body, R)
 
     def step5(k):
@@ -399,7 +464,7 @@ def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev
     return {"workload": f"HeliHover-v0 x {CONFIG5_TOTAL} envs sharded over {world} ranks ({n5} on rank {rank})",
             "with_gather": {"value": CONFIG5_TOTAL * K5 / s_g5, "unit": "env-steps/s",
                             "ms_per_step": s_g5 / K5 * 1e3,
-                            "mode": "eager, dist.gather of obs to rank 0 every step, double-buffered"},
+                            "mode": mode5},
             "without_gather": {"value": CONFIG5_TOTAL * K5 / s_n5, "unit": "env-steps/s",
                                "ms_per_step": s_n5 / K5 * 1e3, "mode": f"hipGraphs of {B} steps"},
             "gather_bytes_per_step_to_rank0": (world - 1) * n5 * 17 * 4, "steps": K5}
@@ -469,10 +534,20 @@ def main():
         off, N = shard_bounds(CONFIG5_TOTAL, rank, world)
         env = make_env(args, torch, N, off, dev)
         bank = action_bank(args, torch, env, N, dev, B)
-        body = gather_loop(torch, dist, env, bank, B, K, rank, world, dev, backend)
-        body(min(args.warmup, K))
+        body = None
+        if backend == "nccl" and os.environ.get("HG_BENCH_CONFIG5_EAGER") != "1":
+            try:
+                body, _keep, G = gather_graphs(torch, dist, env, bank, B, K, rank, world, dev)
+                mode = f"hipGraph (graphs of {G} steps with their dist.gather of obs to rank 0 captured, double-buffered)"
+            except Exception as exc:
+                torch.cuda.synchronize()
+                mode = f"eager (graph capture of the gather failed: {type(exc).__name__}: {exc})"
+        if body is None:
+            body = gather_loop(torch, dist, env, bank, B, K, rank, world, dev, backend)
+            body(min(args.warmup, K))
+            if backend != "nccl" or os.environ.get("HG_BENCH_CONFIG5_EAGER") == "1":
+                mode = "eager (per-step launch + dist.gather to rank 0, double-buffered)"
         sec, secs, wall = timer.run(body, R)
-        mode = "eager (per-step launch + dist.gather to rank 0, double-buffered)"
         total_envs = CONFIG5_TOTAL
     else:
         N = args.envs

@@ -35,6 +35,21 @@ def test_gpus_2_spawns_two_ranks_and_reports_config5():
     assert c5["gather_bytes_per_step_to_rank0"] == 524288 * 17 * 4
 
 
+def test_gpus_8_dry_run():
+    """The driver's scaling run at N = 8: eight ranks, config 5 sharded 131 072 envs per rank (the
+    graph-captured gather needs RCCL; on gloo the eager loop stands in and says so)."""
+    rc, lines, err = run("--gpus", "8")
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["world_size_seen"] == 8
+    assert d["config"]["parallelism"] == "env-shard x8"
+    c5 = d["config5"]
+    assert "131072 on rank 0" in c5["workload"]
+    assert c5["gather_bytes_per_step_to_rank0"] == 7 * 131072 * 17 * 4
+    assert c5["with_gather"]["mode"].startswith("eager")
+
+
 def test_gather_obs_headline_is_config5():
     rc, lines, err = run("--gpus", "2", "--gather-obs")
     assert rc == 0, err[-2000:]
