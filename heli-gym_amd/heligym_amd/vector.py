@@ -44,13 +44,19 @@ class LazyInfo(dict):
     access (then cached).  `valid()` says whether the step's buffers still hold its values; reading
     a field after they were reused raises instead of returning another step's data."""
 
-    def __init__(self, thunks, valid):
+    def __init__(self, thunks, valid, gen=None):
         """thunks: key -> f(info) computing the value (shared between steps: per-step state goes
-        on the info object); valid: () -> bool."""
+        on the info object).  valid: () -> bool; or, with `gen`, the env whose step `gen` this is:
+        the values stay readable while env._gen - gen < 2 (the step's buffer set is not reused
+        before the step after next)."""
         super().__init__(dict.fromkeys(thunks))
         self._thunks = thunks
         self._pending = set(thunks)
-        self._valid = valid
+        self._src = valid
+        self._gen = gen
+
+    def _valid(self):
+        return self._src() if self._gen is None else self._src._gen - self._gen < 2
 
     def _get(self, k):
         if k in self._pending:
@@ -228,6 +234,13 @@ class HeliVecEnv(*_VEC_BASES):
             b["p"] = tuple(b[k].data_ptr() for k in ("info", "index", "final"))
             b["thunks"] = self._info_thunks(b)
             b["thunks_rows"] = self._info_thunks(b, rows=True)
+            # step()'s hg_step_rows arguments after the actions, before the stream
+            b["rows_args"] = (self._p_obs, self._p_rew, self._p_term, self._p_trunc, b["p"][0], None, b["p"][2])
+        self._f32 = torch.float32
+        self._step_rows = self.lib.hg_step_rows
+        # step()'s direct path: same-step auto-reset with reset info (what _launch(rows=True) does),
+        # and a raw-stream accessor to read the current stream with
+        self._rows_fast = self.autoreset and self.autoreset_mode == "same_step" and self._raw_stream is not None
         self._gen = 0
         self._use_set(0)
         # gymnasium.vector's convention: one env's spaces (helicopter.py:56-57) and the batched ones
@@ -372,10 +385,24 @@ class HeliVecEnv(*_VEC_BASES):
         count) only when it is read, which must happen before the step after next.  The reset info
         comes uncompacted (hg_step_rows: the reset envs' info bytes carry HG_INFO_RESET and their
         terminal observations sit at their own rows), so the step is the plain kernel launch."""
+        a = actions
+        # the common call (a float32 [N,4] contiguous tensor on the env's device, in-kernel noise) goes
+        # straight to hg_step_rows with the buffer set's addresses packed at construction: the host
+        # cost per call is then the launch's, not the argument handling's
+        if (eta is None and self._rows_fast and a.dtype is self._f32 and a.is_contiguous()
+                and a.shape == self._act_shape and a.get_device() == self._dev_index):
+            g = self._gen = self._gen + 1
+            b = self._sets[g & 1]
+            self.info_u8 = b["info"]
+            if self.reset_count is not None:   # (only a compacted step fills these)
+                self.reset_count = self.reset_index = self.final_obs = None
+            self._keep = (a, None, None)
+            rc = self._step_rows(self._h, a.data_ptr(), *b["rows_args"], self._raw_stream(self._dev_index))
+            if rc:
+                self._check(rc)
+            return self.obs, self.reward, self._term_b, self._trunc_b, LazyInfo(b["thunks_rows"], self, g)
         b = self._launch(actions, eta, True, None, rows=True)
-        gen = self._gen
-        info = LazyInfo(b["thunks_rows"], lambda: self._gen - gen < 2)
-        return self.obs, self.reward, self._term_b, self._trunc_b, info
+        return self.obs, self.reward, self._term_b, self._trunc_b, LazyInfo(b["thunks_rows"], self, self._gen)
 
     # ------------------------------------------------------------------ setters (helicopter.py:89-111)
     def set_max_time(self, max_time=None):
