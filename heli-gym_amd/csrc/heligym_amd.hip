@@ -1051,17 +1051,24 @@ static inline unsigned retrim_grid(int64_t jobs) {
 #define STEP_KARGS(e) (e)->state, (int64_t)(e)->n, (uint64_t)(e)->cfg.seed, (int64_t)(e)->cfg.env_offset, PARAM_ARG(e), \
                       (e)->tmpl_dev
 
-// Launches with more waves than SIMDs run at most two waves per SIMD: the step kernel fits three
-// (<= 168 VGPRs), but at 4 M envs three run slower (283 us against 272 us per step, HBM-side: the
-// write-heavy stream gains nothing from more requests in flight).  The cap is dynamic LDS that the
-// kernel does not use: 4.25 KB static + 14 KB per one-wave block lets 8 blocks share a CU's 160 KB.
-constexpr size_t kBulkLdsCap = 14 * 1024;
+// Occupancy of launches with more waves than SIMDs.  The step kernel fits three waves per SIMD
+// (<= 168 VGPRs), which is the faster choice while the working set is mostly cache-resident
+// (262 144 forward-flight envs: 21.3 against 25.2 us per step; 1 M: 73.0 against 76.3 us), but past
+// 2 M envs, where the write-heavy HBM stream binds, two waves per SIMD are faster (4 M: 271 against
+// 284 us).  The cap is dynamic LDS the kernel does not use: 4.25 KB static + 14 KB per one-wave
+// block lets 8 blocks share a CU's 160 KB.
+#ifndef HG_BULK_LDS_CAP
+#define HG_BULK_LDS_CAP (14 * 1024)
+#endif
+constexpr size_t kBulkLdsCap = HG_BULK_LDS_CAP;
+constexpr int64_t kBulkCapMinEnvs = 2 * 1024 * 1024;
 
 template <int T, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
 static void launch_step(const hg_env* e, hipStream_t s, const StepArgs& a) {
     const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock);
-    hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED>), dim3(grid), dim3(kStepBlock),
-                       NT ? 0 : kBulkLdsCap, s, STEP_KARGS(e), a);
+    const size_t lds_cap = !NT && e->n >= kBulkCapMinEnvs ? kBulkLdsCap : 0;
+    hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED>), dim3(grid), dim3(kStepBlock), lds_cap, s,
+                       STEP_KARGS(e), a);
 }
 
 // The step variant for a launch: NT when the batch fits one wave per SIMD; the default airframe's
