@@ -35,11 +35,13 @@ for p in (ROOT, os.path.join(ROOT, "heli-gym_amd"), os.path.join(ROOT, "tests"))
 # total itself is 4 B short of its own item list, 29 x 4 + 68 + 4 + 1 + 1 = 190: keeping 318 B makes
 # `achieved` conservative.)
 BYTES_PER_ENV_STEP = 318
-# what the kernel actually moves (bytes the PMC traffic is compared with): reads 136, writes 195
-IMPL_BYTES_PER_ENV_STEP = 136 + 195
+# what the kernel actually moves (bytes the PMC traffic is compared with): reads 128 (state tile
+# 112: heli 16 + wind 5 + carry 4 + counters 3 words, the rotor azimuths are not stepped; action 16),
+# writes 187 (state tile 112, obs 68, reward 4, terminated / truncated / info 3)
+IMPL_BYTES_PER_ENV_STEP = 128 + 187
 # hg_rollout: per step action 16 + obs 68 + reward 4 + flags 2; state + counters once per launch
 ROLLOUT_BYTES_PER_ENV_STEP = 16 + 68 + 4 + 2
-BYTES_STATE_RW = 2 * (108 + 8)
+BYTES_STATE_RW = 2 * 112
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
 REFERENCE_NUMPY_PER_CORE = 1367.0   # env-steps/s/core, reference on config 1
 CONFIG5_TOTAL = 1048576             # BASELINE configs[4]

@@ -4,8 +4,9 @@
 // (Heli.step, heligym/envs/helicopter.py:192-206): Dryden wind RK (k4-only), RK4 of the 18-state
 // helicopter model, task reward, termination flags and same-step auto-reset.  One thread = one
 // env.  Data layout in HBM (all written/read coalesced):
-//   state    wave tiles [ceil(N/64)][30][64] 32-bit words (retrim.h tix): fp32 heli 18 | wind 5 |
-//            carry 4, then the i32 counters (episode step, success steps, episode index)
+//   state    wave tiles [ceil(N/64)][7][64][4] 32-bit words (retrim.h tix): fp32 heli 16 | wind 5 |
+//            carry 4, the i32 counters (episode step, success steps, episode index); the two rotor
+//            azimuths in a per-env record written off the step path (retrim.h AzRec)
 //   actions  [N,4] fp32 (one float4 per lane)      obs [N,17] fp32 (LDS-staged, float4 stores)
 //   reward [N] fp32, terminated/truncated/info [N] u8
 // Model constants are read with scalar loads from a device copy; the terrain map (8 MiB float2
@@ -33,6 +34,7 @@ using hgk::kCtrCol0;
 using hgk::kTileEnvs;
 using hgk::kTileWords;
 using hgk::tix;
+using hgk::AzRec;
 
 namespace {
 
@@ -335,9 +337,9 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     const int64_t i = blk0 + tid;
     const int64_t n = n_p;
     const bool active = i < n;
-    // Addressing: this wave's state tile (8 groups x 64 lanes x 16 bytes, contiguous, retrim.h) from
-    // one uniform (SGPR) base at its middle group, so every group is an immediate offset (-4 .. +3 KB,
-    // inside the 13-bit field) of the same SGPR-base access with the lane's byte offset: no address
+    // Addressing: this wave's state tile (7 groups x 64 lanes x 16 bytes, contiguous, retrim.h) from
+    // one uniform (SGPR) base at group 4, so every group is an immediate offset (-4 .. +2 KB, inside
+    // the 13-bit field) of the same SGPR-base access with the lane's byte offset: no address
     // arithmetic per group.  Lanes past the end of a ragged last tile step its padding and store
     // nothing; for the caller's [N]-row buffers they read row blk0.
     const uint32_t lo = (uint32_t)(active ? tid : 0);
@@ -355,22 +357,21 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     const float tpl = lane < kTplFloats ? reinterpret_cast<const float*>(Tp)[lane] : 0.f;
     // The state groups in the order they are needed (retrim.h slot table): position and step
     // counter (-> terrain texel address, noise key), the rest of the key and the carry, the wind
-    // state (-> wind step), then the heli state.
+    // state (-> wind step), then the heli state.  hs[2], hs[3] (the rotor azimuths) are not stepped.
     float hs[18], ws[5], carry[4];
     int32_t step, succ, epi;
     {
         const f32x4 g0 = ld_lane(GRP(st_b, 0), lt), g1 = ld_lane(GRP(st_b, 1), lt), g2 = ld_lane(GRP(st_b, 2), lt),
                     g3 = ld_lane(GRP(st_b, 3), lt), g4 = ld_lane(GRP(st_b, 4), lt), g5 = ld_lane(GRP(st_b, 5), lt),
                     g6 = ld_lane(GRP(st_b, 6), lt);
-        const f32x2 g7 = ld_lane(reinterpret_cast<const f32x2*>(GRP(st_b, 7)), 2 * lt);
         hs[15] = g0.x; hs[16] = g0.y; hs[17] = g0.z; step = __float_as_int(g0.w);
         epi = __float_as_int(g1.x); succ = __float_as_int(g1.y); carry[3] = g1.z; carry[0] = g1.w;
         carry[1] = g2.x; carry[2] = g2.y; ws[0] = g2.z; ws[1] = g2.w;
-        ws[2] = g3.x; ws[3] = g3.y; ws[4] = g3.z; hs[2] = g3.w;
+        ws[2] = g3.x; ws[3] = g3.y; ws[4] = g3.z; hs[14] = g3.w;
         hs[0] = g4.x; hs[1] = g4.y; hs[4] = g4.z; hs[5] = g4.w;
         hs[6] = g5.x; hs[7] = g5.y; hs[8] = g5.z; hs[9] = g5.w;
         hs[10] = g6.x; hs[11] = g6.y; hs[12] = g6.z; hs[13] = g6.w;
-        hs[14] = g7.x; hs[3] = g7.y;
+        hs[2] = 0.f; hs[3] = 0.f;
     }
     if (FEAT && blockIdx.x == 0 && tid == 0) {   // counters of a later step (rings of three)
         if (a.reset_count_next) *a.reset_count_next = 0;
@@ -422,8 +423,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     // the reference's fp64 arithmetic returns to 1e-16, where the fp32 round trip through x + pi
     // costs up to half an ulp of pi.  The rotor azimuths wrap in nearly every wave every step; the
     // flapping and euler angles only in a wave-uniform branch taken when one of them left the range.
-    hs[2] = in_pi_range(hs[2]) ? hs[2] : hg::pi_bound(hs[2]);
-    hs[3] = in_pi_range(hs[3]) ? hs[3] : hg::pi_bound(hs[3]);
+    // (The rotor azimuths' wrap is az_advance's.)
     {
         const int ang[5] = {4, 5, 12, 13, 14};
         bool all_in = true;
@@ -449,13 +449,14 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
 #else
     const hg::Ground<float> h_post = hg::ground_height(P, a.hmap, hs[15], hs[16]);
 #endif
+    const bool waiting = step < 0;   // ended last step, reset due now (next-step auto-reset)
     step += 1;
     const bool failed = hg::is_failed(P, hs, k, h_post);
     TSTAMP(10, "v"(rew), "v"((int)failed));
     const bool successed = succ >= P.success_steps;   // successed_time before this step's add
     const bool time_up = step >= P.time_up_steps;
-    // next-step auto-reset: an env that ended last step (counter -1) only resets this step
-    const bool pending = FEAT && P.autoreset_next && step == 0;
+    // next-step auto-reset: an env that ended last step (counter -(n + 1)) only resets this step
+    const bool pending = FEAT && P.autoreset_next && waiting;
     const bool term = (failed || successed) && !pending;
     const bool trunc = (time_up || (FEAT && step >= P.max_episode_steps)) && !pending;   // + TimeLimit
     const bool done = term || trunc;
@@ -550,7 +551,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
         carry[1] = obs[5];
         carry[2] = obs[6];
         carry[3] = obs[16];
-        if (FEAT && P.autoreset_next && done) step = -1;   // reset on the next step
+        if (FEAT && P.autoreset_next && done) step = -step - 1;   // reset on the next step (n = step kept)
     }
     store_obs_wave<NT, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, a.obs, so, blk0, n, lane);
     }   // steps
@@ -565,11 +566,10 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
         st_lane<NT>(GRP(st_b, 0), t, f32x4{hs[15], hs[16], hs[17], __int_as_float(step)});
         st_lane<NT>(GRP(st_b, 1), t, f32x4{__int_as_float(epi), __int_as_float(succ), carry[3], carry[0]});
         st_lane<NT>(GRP(st_b, 2), t, f32x4{carry[1], carry[2], ws[0], ws[1]});
-        st_lane<NT>(GRP(st_b, 3), t, f32x4{ws[2], ws[3], ws[4], hs[2]});
+        st_lane<NT>(GRP(st_b, 3), t, f32x4{ws[2], ws[3], ws[4], hs[14]});
         st_lane<NT>(GRP(st_b, 4), t, f32x4{hs[0], hs[1], hs[4], hs[5]});
         st_lane<NT>(GRP(st_b, 5), t, f32x4{hs[6], hs[7], hs[8], hs[9]});
         st_lane<NT>(GRP(st_b, 6), t, f32x4{hs[10], hs[11], hs[12], hs[13]});
-        st_lane<NT>(reinterpret_cast<f32x2*>(GRP(st_b, 7)), 2 * t, f32x2{hs[14], hs[3]});
     }
 #undef GRP
 
@@ -604,16 +604,48 @@ __global__ __launch_bounds__(kBlock) void mask_list_kernel(const uint8_t* mask, 
     if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
 }
 
+// The rotor azimuths (psi_mr, psi_tr): their rates are the constants Omega (helicopter_dynamics.py:
+// 257-258, :288-289), so RK4 adds dt/6 (O + 2 O + 2 O + O) = dt Omega (f_dpsi) per step, and
+// step_after wraps them to [-pi, pi) (:74-75).  The step kernel does not carry them; these are the
+// same fp32 operations it performed on them when they were part of its state, so an azimuth
+// reconstructed from its record is bitwise the one the step would have carried.
+__device__ __forceinline__ float az_wrap(float x) { return in_pi_range(x) ? x : hg::pi_bound(x); }
+
+// The azimuths of an env now, from its record, its counters and its reset template's azimuths
+// (t_mr, t_tr): an episode the record belongs to advances from it, any later episode (begun by an
+// in-kernel auto-reset) from the template at its step 0.
+__device__ float2 az_now(const AzRec& r, int32_t step, int32_t epi, float t_mr, float t_tr, float d_mr, float d_tr) {
+    const int32_t n = hgk::episode_steps(step);
+    float a = t_mr, b = t_tr;
+    int32_t k = n;
+    if (epi == r.epi0 && n >= r.step0) {
+        a = r.mr;
+        b = r.tr;
+        k = n - r.step0;
+    }
+    for (int32_t j = 0; j < k; ++j) {
+        a = az_wrap(a + d_mr);
+        b = az_wrap(b + d_tr);
+    }
+    return make_float2(a, b);
+}
+
+// the reset template's azimuths of env i: the shared template, or the env's own ([N][39])
+__device__ __forceinline__ const float* az_template(const Template<float>* T, const float* tmpl_env, int64_t i) {
+    return tmpl_env ? tmpl_env + i * kTplFloats + hgk::kAzCol0 : T->heli + hgk::kAzCol0;
+}
+
 // Heli.reset for masked envs (helicopter.py:208-217)
 __global__ __launch_bounds__(kBlock) void reset_kernel(const Template<float> T, const float* tmpl_env, float* state,
-                                                       const uint8_t* mask, float* obs, int64_t n) {
+                                                       AzRec* az, const uint8_t* mask, float* obs, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     if (mask && !mask[i]) return;
     // the shared template, or this env's own ([N][39] = heli 18 | carry 4 | obs 17)
     const float* tr = tmpl_env ? tmpl_env + i * kTplFloats : reinterpret_cast<const float*>(&T);
 #pragma unroll
-    for (int c = 0; c < 18; ++c) state[tix(i, c)] = tr[c];
+    for (int c = 0; c < 18; ++c)
+        if (hgk::has_slot(c)) state[tix(i, c)] = tr[c];
 #pragma unroll
     for (int c = 0; c < 5; ++c) state[tix(i, 18 + c)] = 0.f;
 #pragma unroll
@@ -621,7 +653,9 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const Template<float> T, 
     int32_t* ctr = reinterpret_cast<int32_t*>(state);
     ctr[tix(i, kCtrCol0 + 0)] = 0;
     ctr[tix(i, kCtrCol0 + 1)] = 0;
-    ctr[tix(i, kCtrCol0 + 2)] += 1;
+    const int32_t epi = ctr[tix(i, kCtrCol0 + 2)] + 1;
+    ctr[tix(i, kCtrCol0 + 2)] = epi;
+    az[i] = AzRec{tr[hgk::kAzCol0], tr[hgk::kAzCol0 + 1], 0, epi};
     if (obs) {
 #pragma unroll
         for (int c = 0; c < 17; ++c) obs[i * 17 + c] = tr[22 + c];
@@ -629,27 +663,74 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(const Template<float> T, 
 }
 
 // every slot of every tile, the padding of a ragged last tile included (its lanes step like the
-// others and store nothing)
-__global__ __launch_bounds__(kBlock) void init_kernel(const Template<float> T, float* state, int64_t slots) {
+// others and store nothing); the azimuth record of every env
+__global__ __launch_bounds__(kBlock) void init_kernel(const Template<float> T, float* state, int64_t slots, AzRec* az,
+                                                      int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= slots) return;
-    for (int c = 0; c < 18; ++c) state[tix(i, c)] = T.heli[c];
+    for (int c = 0; c < 18; ++c)
+        if (hgk::has_slot(c)) state[tix(i, c)] = T.heli[c];
     for (int c = 0; c < 5; ++c) state[tix(i, 18 + c)] = 0.f;
     for (int c = 0; c < 4; ++c) state[tix(i, 23 + c)] = T.carry[c];
     int32_t* ctr = reinterpret_cast<int32_t*>(state);
     for (int c = 0; c < 3; ++c) ctr[tix(i, kCtrCol0 + c)] = 0;
+    if (i < n) az[i] = AzRec{T.heli[hgk::kAzCol0], T.heli[hgk::kAzCol0 + 1], 0, 0};
 }
 
-// tiles <-> [N, cols] records for get/set_state: columns c0 .. c0+cols-1 of the tiles (32-bit words)
-__global__ void tiles_to_rows(const uint32_t* tiles, uint32_t* rows, int c0, int cols, int64_t n) {
+// tiles -> [N, 27] state / [N, 3] counter records (get_state); the azimuths reconstructed, the step
+// counter of an env waiting for its next-step reset exported as -1
+__global__ __launch_bounds__(kBlock) void get_rows_kernel(const uint32_t* tiles, const AzRec* az,
+                                                          const Template<float>* T, const float* tmpl_env,
+                                                          const Params<float>* P, uint32_t* state_rows,
+                                                          int32_t* counter_rows, int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    for (int c = 0; c < cols; ++c) rows[i * cols + c] = tiles[tix(i, c0 + c)];
+    const int32_t* ctr = reinterpret_cast<const int32_t*>(tiles);
+    const int32_t step = ctr[tix(i, kCtrCol0 + 0)], epi = ctr[tix(i, kCtrCol0 + 2)];
+    if (state_rows) {
+        for (int c = 0; c < kStateCols; ++c)
+            if (hgk::has_slot(c)) state_rows[i * kStateCols + c] = tiles[tix(i, c)];
+        const float* ta = az_template(T, tmpl_env, i);
+        const float2 a = az_now(az[i], step, epi, ta[0], ta[1], P->f_dpsi_mr, P->f_dpsi_tr);
+        state_rows[i * kStateCols + hgk::kAzCol0] = __float_as_uint(a.x);
+        state_rows[i * kStateCols + hgk::kAzCol0 + 1] = __float_as_uint(a.y);
+    }
+    if (counter_rows) {
+        counter_rows[i * kCtrCols + 0] = step < 0 ? -1 : step;
+        counter_rows[i * kCtrCols + 1] = ctr[tix(i, kCtrCol0 + 1)];
+        counter_rows[i * kCtrCols + 2] = epi;
+    }
 }
-__global__ void rows_to_tiles(const uint32_t* rows, uint32_t* tiles, int c0, int cols, int64_t n) {
+
+// [N, 27] / [N, 3] records -> tiles (set_state; either may be NULL): the azimuth record is rewritten
+// at the env's (new) counters, with the given azimuths or the current ones (both NULL: the
+// azimuths are re-anchored in place, before a reset template changes)
+__global__ __launch_bounds__(kBlock) void set_rows_kernel(uint32_t* tiles, AzRec* az, const Template<float>* T,
+                                                          const float* tmpl_env, const Params<float>* P,
+                                                          const uint32_t* state_rows, const int32_t* counter_rows,
+                                                          int64_t n) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    for (int c = 0; c < cols; ++c) tiles[tix(i, c0 + c)] = rows[i * cols + c];
+    int32_t* ctr = reinterpret_cast<int32_t*>(tiles);
+    int32_t step = ctr[tix(i, kCtrCol0 + 0)], epi = ctr[tix(i, kCtrCol0 + 2)];
+    float2 a;
+    if (state_rows) {
+        a = make_float2(__uint_as_float(state_rows[i * kStateCols + hgk::kAzCol0]),
+                        __uint_as_float(state_rows[i * kStateCols + hgk::kAzCol0 + 1]));
+        for (int c = 0; c < kStateCols; ++c)
+            if (hgk::has_slot(c)) tiles[tix(i, c)] = state_rows[i * kStateCols + c];
+    } else {
+        const float* ta = az_template(T, tmpl_env, i);
+        a = az_now(az[i], step, epi, ta[0], ta[1], P->f_dpsi_mr, P->f_dpsi_tr);
+    }
+    if (counter_rows) {
+        step = counter_rows[i * kCtrCols + 0];
+        epi = counter_rows[i * kCtrCols + 2];
+        ctr[tix(i, kCtrCol0 + 0)] = step;
+        ctr[tix(i, kCtrCol0 + 1)] = counter_rows[i * kCtrCols + 1];
+        ctr[tix(i, kCtrCol0 + 2)] = epi;
+    }
+    az[i] = AzRec{a.x, a.y, hgk::episode_steps(step), epi};
 }
 
 __global__ __launch_bounds__(kBlock) void random_actions_kernel(float* act, int64_t n, int64_t env_offset,
@@ -953,6 +1034,7 @@ struct hg_env {
     std::vector<float2> hmap_host;   // {hi, lo} split of the fp64 heights
     float2* hmap = nullptr;
     float* state = nullptr;                 // wave tiles (retrim.h tix): state columns + counters
+    AzRec* az = nullptr;                    // rotor azimuth records [N] (retrim.h AzRec)
     Params<float> Pf;
     Params<double> Pd;
     Template<float> tmpl;
@@ -1016,6 +1098,19 @@ static int32_t upload_params(hg_env* e) {
     return HG_OK;
 }
 
+static inline unsigned grid_for(int64_t n);
+// Re-anchor every env's azimuth record at its current counters (before a reset template changes:
+// the records of episodes begun by an in-kernel reset point at the template).  Synchronous.
+static hipError_t reanchor_azimuths(hg_env* e) {
+    if (!e->az) return hipSuccess;
+    hipLaunchKernelGGL(set_rows_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, 0, reinterpret_cast<uint32_t*>(e->state),
+                       e->az, e->tmpl_dev, e->Pf.env_templates ? e->tmpl_env : nullptr,
+                       (const Params<float>*)e->params_dev, nullptr, nullptr, e->n);
+    hipError_t err = hipGetLastError();
+    if (err == hipSuccess) err = hipDeviceSynchronize();
+    return err;
+}
+
 static int32_t build_template(hg_env* e) {
     const double W[3] = {e->Pd.wm[0], e->Pd.wm[1], e->Pd.wm[2]};   // helicopter.py:55 (mean wind)
     hg_trim_result r;
@@ -1032,6 +1127,7 @@ static int32_t build_template(hg_env* e) {
     e->setup = trim_setup(e->Pd, e->hmap_host.data(), e->cfg.trim);
     if (e->tmpl_dev) {   // device copies read by the step / re-trim kernels (after all queued work)
         hipError_t err = hipDeviceSynchronize();
+        if (err == hipSuccess) err = reanchor_azimuths(e);   // (they may start from the old template's)
         if (err == hipSuccess) err = hipMemcpy(e->tmpl_dev, &e->tmpl, sizeof(e->tmpl), hipMemcpyHostToDevice);
         if (err == hipSuccess && e->setup_dev)
             err = hipMemcpy(e->setup_dev, &e->setup, sizeof(e->setup), hipMemcpyHostToDevice);
@@ -1223,7 +1319,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     rc = build_template(e);
     if (rc != HG_OK) { delete e; return rc; }
     auto cleanup = [&](hipError_t err, const char* what) {
-        dfree(e->hmap); dfree(e->state); dfree(e->tmpl_dev); dfree(e->params_dev);
+        dfree(e->hmap); dfree(e->state); dfree(e->az); dfree(e->tmpl_dev); dfree(e->params_dev);
         dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_count);
         dfree(e->retrim_ring);
         dfree(e->tmpl_env); dfree(e->setup_batch);
@@ -1240,6 +1336,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if ((err = hipMalloc(&e->hmap, sizeof(float2) * rows * cols)) != hipSuccess) return cleanup(err, "hipMalloc terrain");
     if ((err = hipMalloc(&e->state, sizeof(float) * hgk::tile_words(num_envs))) != hipSuccess)
         return cleanup(err, "hipMalloc state");
+    if ((err = hipMalloc(&e->az, sizeof(AzRec) * num_envs)) != hipSuccess) return cleanup(err, "hipMalloc azimuths");
     if ((err = hipMemcpy(e->hmap, e->hmap_host.data(), sizeof(float2) * rows * cols, hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy terrain");
     if ((err = hipMalloc(&e->params_dev, sizeof(Params<float>))) != hipSuccess) return cleanup(err, "hipMalloc params");
@@ -1268,7 +1365,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
         if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "fill_wind_kernel");
     }
     const int64_t slots = hgk::tile_words(num_envs) / hgk::kEnvSlots;
-    hipLaunchKernelGGL(init_kernel, dim3(grid_for(slots)), dim3(kBlock), 0, 0, e->tmpl, e->state, slots);
+    hipLaunchKernelGGL(init_kernel, dim3(grid_for(slots)), dim3(kBlock), 0, 0, e->tmpl, e->state, slots, e->az,
+                       num_envs);
     if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "init_kernel");
     if ((err = hipDeviceSynchronize()) != hipSuccess) return cleanup(err, "init sync");
     *out = e;
@@ -1280,6 +1378,7 @@ void hg_destroy(hg_env* e) {
     DevGuard dev_guard(e);
     dfree(e->hmap);
     dfree(e->state);
+    dfree(e->az);
     dfree(e->tmpl_dev);
     dfree(e->params_dev);
     dfree(e->setup_dev);
@@ -1343,7 +1442,7 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(reset_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, e->tmpl,
-                       e->Pf.env_templates ? e->tmpl_env : nullptr, e->state, mask, obs, e->n);
+                       e->Pf.env_templates ? e->tmpl_env : nullptr, e->state, e->az, mask, obs, e->n);
     HIP_TRY(hipGetLastError());
     if (e->cfg.reset_mode == HG_RESET_RETRIM) {   // trim each masked env against its last wind (F8)
         HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
@@ -1357,6 +1456,7 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
         r.list = e->retrim_list;
         r.wind = e->retrim_wind;
         r.state = e->state;
+        r.az = e->az;
         r.obs = obs;
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
@@ -1441,6 +1541,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.list = e->retrim_list;
         r.wind = e->retrim_wind;
         r.state = e->state;
+        r.az = e->az;
         r.obs = obs;
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
@@ -1567,6 +1668,8 @@ int32_t hg_set_reset_templates(hg_env* e, const float* templates, void* stream) 
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (templates && e->cfg.reset_mode == HG_RESET_RETRIM)
         return fail(HG_E_INVALID, "per-env reset templates need reset_mode HG_RESET_TEMPLATE");
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(reanchor_azimuths(e));   // the records may point at the templates being replaced
     if (templates) {
         if (!e->tmpl_env) HIP_TRY(hipMalloc(&e->tmpl_env, sizeof(float) * kTplFloats * e->n));
         HIP_TRY(hipMemcpyAsync(e->tmpl_env, templates, sizeof(float) * kTplFloats * e->n, hipMemcpyDeviceToDevice,
@@ -1592,13 +1695,10 @@ int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
-    hipStream_t s = (hipStream_t)stream;
-    uint32_t* t = reinterpret_cast<uint32_t*>(e->state);
-    if (state)
-        hipLaunchKernelGGL(tiles_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, t, (uint32_t*)state, 0, kStateCols, e->n);
-    if (counters)
-        hipLaunchKernelGGL(tiles_to_rows, dim3(grid_for(e->n)), dim3(kBlock), 0, s, t, (uint32_t*)counters, kCtrCol0,
-                           kCtrCols, e->n);
+    if (!state && !counters) return HG_OK;
+    hipLaunchKernelGGL(get_rows_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<const uint32_t*>(e->state), e->az, e->tmpl_dev,
+                       e->Pf.env_templates ? e->tmpl_env : nullptr, PARAM_ARG(e), (uint32_t*)state, counters, e->n);
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }
@@ -1607,14 +1707,11 @@ int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, voi
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
-    hipStream_t s = (hipStream_t)stream;
-    uint32_t* t = reinterpret_cast<uint32_t*>(e->state);
-    if (state)
-        hipLaunchKernelGGL(rows_to_tiles, dim3(grid_for(e->n)), dim3(kBlock), 0, s, (const uint32_t*)state, t, 0, kStateCols,
-                           e->n);
-    if (counters)
-        hipLaunchKernelGGL(rows_to_tiles, dim3(grid_for(e->n)), dim3(kBlock), 0, s, (const uint32_t*)counters, t, kCtrCol0,
-                           kCtrCols, e->n);
+    if (!state && !counters) return HG_OK;
+    hipLaunchKernelGGL(set_rows_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream,
+                       reinterpret_cast<uint32_t*>(e->state), e->az, e->tmpl_dev,
+                       e->Pf.env_templates ? e->tmpl_env : nullptr, PARAM_ARG(e), (const uint32_t*)state, counters,
+                       e->n);
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }

@@ -10,30 +10,47 @@
 
 namespace hgk {
 
-// Env state in HBM: wave tiles of 64 envs, [ceil(N/64)][8][64][4] 32-bit words.  An env has 32
-// slots in eight groups of four; group g of a tile is 64 lanes x 16 bytes, so the step kernel moves a
-// group with one 16-byte access per lane, 1 KB contiguous per wave (8 loads and 8 stores per env
-// instead of 30 of 4 bytes).  The 30 logical columns -- the fp32 state record 0..26 (heli 18 | wind 5
+// Env state in HBM: wave tiles of 64 envs, [ceil(N/64)][7][64][4] 32-bit words.  An env has 28
+// slots in seven groups of four; group g of a tile is 64 lanes x 16 bytes, so the step kernel moves a
+// group with one 16-byte access per lane, 1 KB contiguous per wave (7 loads and 7 stores per env
+// instead of 28 of 4 bytes).  The 30 logical columns -- the fp32 state record 0..26 (heli 18 | wind 5
 // | carry 4) and the int32 counters 27..29 (episode step, success steps, episode index) -- sit in the
 // groups in the order the step needs them: position and step counter, the noise key and carry, the
-// wind state, then the heli state; slots 30 and 31 are padding, never read or written by the step.
+// wind state, then the heli state.  Columns 2 and 3, the rotor azimuths, have no slot: no force,
+// observation, reward or flag reads them (helicopter_dynamics.py:203-300 take psi_mr / psi_tr and
+// never use them) and each advances by the constant dt * Omega per step (:257-258, :288-289), so
+// they live in an azimuth record per env (AzRec, below) and are reconstructed when the state is read.
+// The step counter of an env waiting for its next-step auto-reset is -(n + 1), n = the steps its
+// episode took (exported as -1).
 constexpr int kTileEnvs = 64;
 static_assert(HG_STATE_COLS + HG_COUNTER_COLS == 30, "the slot table covers 30 columns");
 constexpr int kCtrCol0 = HG_STATE_COLS;
 constexpr int kTileCols = HG_STATE_COLS + HG_COUNTER_COLS;   // logical columns
-constexpr int kEnvSlots = 32;
+constexpr int kEnvSlots = 28;
 constexpr int kTileWords = kEnvSlots * kTileEnvs;
-// slot of logical column c:  x y z step | epi succ carry3 carry0 | carry1 carry2 ws0 ws1 |
-// ws2 ws3 ws4 psi_mr | vi_mr vi_tr b0 b1 | u v w p | q r phi theta | psi psi_tr - -
+constexpr int kAzCol0 = 2;   // psi_mr, psi_tr: the columns without a slot
+// slot of logical column c (-1: an azimuth):  x y z step | epi succ carry3 carry0 |
+// carry1 carry2 ws0 ws1 | ws2 ws3 ws4 psi | vi_mr vi_tr b0 b1 | u v w p | q r phi theta
 __host__ __device__ constexpr int slot_of(int c) {
-    constexpr int t[30] = {16, 17, 15, 29, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 0, 1, 2,
+    constexpr int t[30] = {16, 17, -1, -1, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 15, 0, 1, 2,
                            10, 11, 12, 13, 14, 7, 8, 9, 6, 3, 5, 4};
     return t[c];
 }
-__host__ __device__ inline int64_t tix(int64_t env, int col) {
+__host__ __device__ inline int64_t tix(int64_t env, int col) {   // (col not an azimuth)
     const int s = slot_of(col);
     return (env / kTileEnvs) * kTileWords + (s >> 2) * (4 * kTileEnvs) + (env % kTileEnvs) * 4 + (s & 3);
 }
+__host__ __device__ inline bool has_slot(int col) { return slot_of(col) >= 0; }
+
+// Azimuth record of an env: the rotor azimuths (mr, tr) at step `step0` of episode `epi0`.  Written
+// only off the step path (create, reset, set_state, a re-trim, before a template change); an episode
+// begun by an in-kernel auto-reset (episode index != epi0) starts from its reset template's azimuths.
+struct AzRec {
+    float mr, tr;
+    int32_t step0, epi0;
+};
+// steps an env's episode has taken, from its step counter (negative: waiting for its next-step reset)
+__host__ __device__ inline int32_t episode_steps(int32_t step) { return step >= 0 ? step : -step - 1; }
 inline int64_t tile_words(int64_t n) { return ((n + kTileEnvs - 1) / kTileEnvs) * kTileWords; }
 
 struct RetrimArgs {
@@ -45,6 +62,7 @@ struct RetrimArgs {
     const int32_t* list;    // env mode: env id of each job
     const float* wind;      // [N,3] by env id (env mode) or [count,3] by job (batch mode)
     float* state;           // env mode: tiled state (tix; heli 18 and carry 4 rewritten)
+    AzRec* az;              // env mode: azimuth records (the trim's azimuths at step 0)
     float* obs;             // env mode: [N,17] reset observation rows, or NULL
     int64_t n;
     float* out_state;       // batch mode outputs (rows by job), each may be NULL

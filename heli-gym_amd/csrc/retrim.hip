@@ -188,7 +188,10 @@ __device__ __forceinline__ bool gauss_jordan_wave(const double* E, const double*
 __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, int64_t env, const double x[16],
                                              const double s[18], const double ob[17]) {
     if (a.list) {
-        for (int c = 0; c < 18; ++c) a.state[tix(env, c)] = (float)s[c];
+        for (int c = 0; c < 18; ++c)
+            if (has_slot(c)) a.state[tix(env, c)] = (float)s[c];
+        const int32_t epi = reinterpret_cast<const int32_t*>(a.state)[tix(env, kCtrCol0 + 2)];
+        a.az[env] = AzRec{(float)s[kAzCol0], (float)s[kAzCol0 + 1], 0, epi};   // the reset's step 0
         const int co[4] = {4, 5, 6, 16};
         for (int c = 0; c < 4; ++c) a.state[tix(env, 23 + c)] = (float)ob[co[c]];
         if (a.obs)

@@ -10,7 +10,7 @@
 //    stall branches (:322-361), the flapping equations (:236-262), the plane rotations of the DCM
 //    (kinematic.py:3-17), the RK4 combinations.  The stage state is held as pairs
 //    (vi_mr, vi_tr) (b0, b1) (u, v) (w, z) (p, q) (r, theta) (phi, psi) (x, y); the rotor
-//    azimuths, which no force model reads, advance by dt * Omega once per step.
+//    azimuths, which no force model reads, are not part of the stepped state (az_advance).
 //  * Work moved out of the stages.  The ISA density (:160-165) and the main rotor's density
 //    terms (the flapping time constants ITB, ITB2_OM, :214-221) are evaluated once per step at the
 //    committed altitude z0 and linearised in z - z0 (the stage altitudes differ from z0 by
@@ -548,10 +548,7 @@ HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict
     stage_f32<true>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     rk_update2(h, k, acc, P.dt6);
     from_x16(h, hs);
-    // rotor azimuths: constant rates (:457-458), dt / 6 (O + 2 O + 2 O + O) = dt O
-    const f2 psi = f2{hs[2], hs[3]} + f2{P.f_dpsi_mr, P.f_dpsi_tr};
-    hs[2] = psi.x;
-    hs[3] = psi.y;
+    // (the rotor azimuths hs[2], hs[3] are not stepped here: see az_advance)
     from_x16(k, d);
     d[2] = P.mr_OMEGA;
     d[3] = P.tr_OMEGA;
