@@ -57,7 +57,7 @@ if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     out["traffic_note"] = ("2*FETCH_SIZE + WRITE_SIZE (KiB*1024), the gfx950 FETCH_SIZE x2 correction, checked for "
                            "this kernel's 4-B and 16-B-per-lane accesses on known byte counts in "
                            "profiles/*_pmc_calibration.json")
-    out["impl_bytes_per_launch"] = n * (136 + 195)
+    out["impl_bytes_per_launch"] = n * (128 + 187)   # bench.py IMPL_BYTES_PER_ENV_STEP
     out["algorithmic_bytes_per_launch"] = n * 318
 with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as f:
     json.dump(out, f, indent=1)
