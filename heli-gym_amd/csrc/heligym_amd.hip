@@ -1147,23 +1147,14 @@ static inline unsigned retrim_grid(int64_t jobs) {
 #define STEP_KARGS(e) (e)->state, (int64_t)(e)->n, (uint64_t)(e)->cfg.seed, (int64_t)(e)->cfg.env_offset, PARAM_ARG(e), \
                       (e)->tmpl_dev
 
-// Occupancy of launches with more waves than SIMDs.  The step kernel fits three waves per SIMD
-// (<= 168 VGPRs), which is the faster choice while the working set is mostly cache-resident
-// (262 144 forward-flight envs: 21.3 against 25.2 us per step; 1 M: 73.0 against 76.3 us), but past
-// 2 M envs, where the write-heavy HBM stream binds, two waves per SIMD are faster (4 M: 271 against
-// 284 us).  The cap is dynamic LDS the kernel does not use: 4.25 KB static + 14 KB per one-wave
-// block lets 8 blocks share a CU's 160 KB.
-#ifndef HG_BULK_LDS_CAP
-#define HG_BULK_LDS_CAP (14 * 1024)
-#endif
-constexpr size_t kBulkLdsCap = HG_BULK_LDS_CAP;
-constexpr int64_t kBulkCapMinEnvs = 2 * 1024 * 1024;
-
+// Occupancy of launches with more waves than SIMDs: three waves per SIMD (<= 168 VGPRs) at every
+// size.  Until the azimuths left the stepped state, two waves per SIMD (a dynamic-LDS cap) were
+// faster past 2 M envs, where the write-heavy HBM stream binds (4 M: 271 against 284 us); with the
+// 28-word tile three are (4 M: 254.6 against 257.8 us, interleaved A/B), so the cap is gone.
 template <int T, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
 static void launch_step(const hg_env* e, hipStream_t s, const StepArgs& a) {
     const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock);
-    const size_t lds_cap = !NT && e->n >= kBulkCapMinEnvs ? kBulkLdsCap : 0;
-    hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED>), dim3(grid), dim3(kStepBlock), lds_cap, s,
+    hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED>), dim3(grid), dim3(kStepBlock), 0, s,
                        STEP_KARGS(e), a);
 }
 
