@@ -592,10 +592,11 @@ def main():
                     for k in range(Ke):
                         env.step(bank[k % B])
                 eager_api()
-                s_api, _, _ = timer.run(eager_api, 1)
+                s_api, s_api_all, _ = timer.run(eager_api, 5)   # median of 5 windows (host jitter)
                 secondary["step_api_eager"] = {
                     "value": total_envs * Ke / s_api, "unit": "env-steps/s", "ms_per_step": s_api / Ke * 1e3,
-                    "steps": Ke, "note": "HeliVecEnv.step() as an RL loop calls it: eager launch of the plain "
+                    "steps": Ke, "windows_s": s_api_all,
+                    "note": "HeliVecEnv.step() as an RL loop calls it: eager launch of the plain "
                                          "kernel (hg_step_rows: reset envs flagged in the info bytes, their "
                                          "terminal observations at their own rows); its info dict is lazy "
                                          "(fields not read here; the reset info costs one nonzero when read)"}
