@@ -50,7 +50,7 @@ struct AzRec {
     int32_t step0, epi0;
 };
 // steps an env's episode has taken, from its step counter (negative: waiting for its next-step reset)
-__host__ __device__ inline int32_t episode_steps(int32_t step) { return step >= 0 ? step : -step - 1; }
+__host__ __device__ inline int32_t episode_steps(int32_t step) { return step >= 0 ? step : -(step + 1); }
 inline int64_t tile_words(int64_t n) { return ((n + kTileEnvs - 1) / kTileEnvs) * kTileWords; }
 
 struct RetrimArgs {

@@ -19,14 +19,18 @@ MAX_EPISODE_STEPS = 5000   # heligym/__init__.py:4-18
 REWARD_THRESHOLD = 0.95
 
 
-def make_vec(env_id, num_envs, autoreset_mode="next_step", max_episode_steps=MAX_EPISODE_STEPS, **kwargs):
+def make_vec(env_id, num_envs, autoreset_mode="next_step", max_episode_steps=MAX_EPISODE_STEPS,
+             reset_mode="retrim", **kwargs):
     """`gymnasium.make_vec(env_id, num_envs)` for the heligym ids: one batched GPU env with the
-    registry's TimeLimit (max_episode_steps=5000) and gymnasium's vector autoreset default
-    (next step); kwargs go to HeliVecEnv (dt, seed, device, reset_mode, trim_cond, ...)."""
+    registry's TimeLimit (max_episode_steps=5000), gymnasium's vector autoreset default (next step)
+    and the reference's resets: every reset re-trimmed against the env's last wind, as N reference
+    envs in a gymnasium vector env reset (helicopter.py:208-212; reset_mode="template" is the
+    faster mean-wind template); kwargs go to HeliVecEnv (dt, seed, device,
+    trim_cond, ...)."""
     if env_id not in ENV_IDS:
         raise ValueError(f"unknown env id {env_id!r}; one of {sorted(ENV_IDS)}")
     env = HeliVecEnv(num_envs, task=ENV_IDS[env_id], autoreset=True, autoreset_mode=autoreset_mode,
-                     max_episode_steps=max_episode_steps, **kwargs)
+                     max_episode_steps=max_episode_steps, reset_mode=reset_mode, **kwargs)
     env.spec_id = env_id
     env.reward_threshold = REWARD_THRESHOLD
     return env

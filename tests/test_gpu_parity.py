@@ -845,7 +845,11 @@ def test_make_vec_registry_defaults(torch):
     env = heligym_amd.make_vec("HeliHover-v0", 64, dt=0.02)
     assert env.task == "hover" and env.autoreset_mode == "next_step" and env.max_episode_steps == 5000
     assert env.cfg.max_episode_steps == 5000 and env.reward_threshold == 0.95
+    assert env.reset_mode == "retrim"   # the reference's resets (F8) by default
     env.close()
+    fast = heligym_amd.make_vec("HeliHover-v0", 64, dt=0.02, reset_mode="template")
+    assert fast.reset_mode == "template"
+    fast.close()
 
 
 @pytest.mark.parametrize("opts", [dict(), dict(eta=True), dict(max_episode_steps=37),
