@@ -15,6 +15,9 @@ namespace {
 #ifndef HG_TIMING
 #define HG_TIMING 0
 #endif
+#ifndef HG_GJ_FLOW   // Gauss-Jordan pivot steps without per-step early exits (see gj_step)
+#define HG_GJ_FLOW 1
+#endif
 #if HG_TIMING
 // diagnostic build: s_memtime at the phase boundaries of the first job's rounds (lane 0)
 __device__ unsigned long long g_rt_timing[64];
@@ -140,8 +143,15 @@ __device__ __forceinline__ bool gj_step(double (&a)[5], int& pos, int l, bool st
     // the host's first candidate M[C][C] being NaN keeps it as the (non-finite) pivot
     const bool c_nan = __ballot(q == qc && pos == C && nan_v) != 0;
     GJSTAMP(1, "s"(P));
-    if (!hit || c_nan || mp == 0.0 || !isfinite(mp)) return false;
+    const bool bad = !hit || c_nan || mp == 0.0 || !isfinite(mp);
+#if HG_GJ_FLOW
+    // No branch on a failed pivot step: it is reported after the last step (the steps in between
+    // compute values nobody reads), so a step's remaining eliminations and the next step's pivot
+    // search share a basic block and the scheduler overlaps them.
+#else
+    if (bad) return false;
     __builtin_amdgcn_sched_barrier(0);   // the pivot-row reads are in flight during the division
+#endif
     const double rinv = 1.0 / mp;
 #pragma unroll
     for (int t = 0; t < 5; ++t) pr[t] *= rinv;
@@ -154,13 +164,22 @@ __device__ __forceinline__ bool gj_step(double (&a)[5], int& pos, int l, bool st
     }
     pos = pos == ppos ? C : (pos == C ? ppos : pos);
     GJSTAMP(3, "v"(a[0]), "v"(a[4]));
-    return true;
+    return !bad;
 }
 template <int C>
 __device__ __forceinline__ bool gj_steps(double (&a)[5], int& pos, int l, bool stamp) {
+#if HG_GJ_FLOW
+    const bool ok = gj_step<C>(a, pos, l, stamp);
+    if constexpr (C < 15) {
+        const bool rest = gj_steps<C + 1>(a, pos, l, stamp);
+        return ok && rest;
+    }
+    return ok;
+#else
     if (!gj_step<C>(a, pos, l, stamp)) return false;
     if constexpr (C < 15) return gj_steps<C + 1>(a, pos, l, stamp);
     return true;
+#endif
 }
 
 // The Newton system arrives in LDS as the raw evaluations: E[j][k] = y_k at x + eps e_j (j < 16) and
