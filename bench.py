@@ -45,7 +45,7 @@ BYTES_STATE_RW = 2 * 112
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md (spec; 6.3 TB/s measured copy)
 REFERENCE_NUMPY_PER_CORE = 1367.0   # env-steps/s/core, reference on config 1
 CONFIG5_TOTAL = 1048576             # BASELINE configs[4]
-OUT_OF_CACHE_ENVS = 4194304         # 1.39 GB moved per launch: past the 256 MB Infinity Cache
+OUT_OF_CACHE_ENVS = 4194304         # 1.32 GB moved per launch: past the 256 MB Infinity Cache
 
 
 def parse():
@@ -649,7 +649,7 @@ def main():
             envr.close()
 
         if world == 1 and not args.no_secondary and not args.dry_run and args.envs < OUT_OF_CACHE_ENVS:
-            # the same step past the 256 MB Infinity Cache (1.39 GB moved per launch): HBM bytes, not
+            # the same step past the 256 MB Infinity Cache (1.32 GB moved per launch): HBM bytes, not
             # fabric bytes, with its own committed PMC summary
             Nx = OUT_OF_CACHE_ENVS
             envx = make_env(args, torch, Nx, 0, dev)
@@ -669,7 +669,7 @@ def main():
                 "steps": Kx, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
                 "traffic": (pmc_traffic(Nx, args.dt, args.task) or (None,))[0],
                 "traffic_source": (pmc_traffic(Nx, args.dt, args.task) or (None, None))[1],
-                "note": "working set 1.39 GB per launch, past the 256 MB MALL: the traffic is HBM bytes"}
+                "note": "working set 1.32 GB per launch, past the 256 MB MALL: the traffic is HBM bytes"}
             envx.close()
             del bankx
 
