@@ -282,9 +282,10 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
                 first = false;
                 have_jac = true;
             } else {
-                int js = hg::kTrimLineSearch;
-                for (int jj = hg::kTrimLineSearch - 1; jj >= 0; --jj)
-                    if (read_lane(te, 32 + jj) < tol) js = jj;
+                // the first trial (lanes 32 + j) whose residual is below tol: one ballot instead of a
+                // readlane per trial (the reference's sequential search, helicopter_dynamics.py:532-541)
+                const unsigned long long lower = __ballot(j >= 0 && j < hg::kTrimLineSearch && te < tol) >> 32;
+                const int js = lower ? __builtin_ctzll(lower) : hg::kTrimLineSearch;
                 if (js >= hg::kTrimLineSearch - 1) {   // helicopter_dynamics.py:540: keep x
                     done = true;
                     src = -1;
