@@ -123,6 +123,9 @@ struct StepArgs {
 // ~0.6 KB of kernel arguments and spill more SGPRs.
 using ParamArg = const Params<float>* __restrict__;
 
+#ifndef HG_NT_WAVES   // the lone-wave (NT) variant up to this many waves per SIMD
+#define HG_NT_WAVES 2
+#endif
 #ifndef HG_MIN_WAVES
 #define HG_MIN_WAVES 1
 #endif
@@ -1172,7 +1175,7 @@ static void dispatch_step(const hg_env* e, hipStream_t s, const StepArgs& a, boo
             else eta ? launch_step<T, true, NT, false, MULTI, false>(e, s, a) : launch_step<T, false, NT, false, MULTI, false>(e, s, a);
         }
     };
-    if (e->n <= e->resident_envs) pick(std::true_type{});
+    if (e->n <= HG_NT_WAVES * e->resident_envs) pick(std::true_type{});
     else pick(std::false_type{});
 }
 template <bool MULTI>
