@@ -123,6 +123,9 @@ struct StepArgs {
 // ~0.6 KB of kernel arguments and spill more SGPRs.
 using ParamArg = const Params<float>* __restrict__;
 
+#ifndef HG_NTS_WAVES   // bulk per-step launches store non-temporally up to this many waves per SIMD
+#define HG_NTS_WAVES 4
+#endif
 #ifndef HG_NT_WAVES   // the lone-wave (NT) variant up to this many waves per SIMD
 #define HG_NT_WAVES 2
 #endif
@@ -322,11 +325,12 @@ namespace {
 // kept in registers between them; BAKED: the default airframe's model constants compiled in as
 // instruction literals (baked.h), the runtime fields still read from the device copy.  All
 // compile-time, so the hot kernel has no data-independent branches to merge around.
-template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
+template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool NTS>
 __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p,
                                                       int64_t envoff_p, ParamArg Pa,
                                                       const Template<float>* __restrict__ Tp, const StepArgs a) {
     __shared__ float s_obs[kStepBlock * HG_N_OBS];   // one 64-row slice per wave
+    constexpr bool kNTS = NT || NTS;   // non-temporal output stores
     const Params<float>& P0 = *Pa;   // model constants: scalar loads from a device copy
     // BAKED: the default airframe's constants as instruction literals (baked.h); only the runtime
     // fields (dt, target, limits, flags) are loaded
@@ -468,11 +472,11 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     // auto-reset (same step, or the step after the end)
     const bool do_reset = P.autoreset && active && ((FEAT && P.autoreset_next) ? pending : done);
     if (active) {
-        st_lane<NT>(a.reward + so + blk0, (uint32_t)tid, pending ? 0.f : rew);
-        st_lane<NT>(a.terminated + so + blk0, (uint32_t)tid, (uint8_t)term);
-        st_lane<NT>(a.truncated + so + blk0, (uint32_t)tid, (uint8_t)trunc);
+        st_lane<kNTS>(a.reward + so + blk0, (uint32_t)tid, pending ? 0.f : rew);
+        st_lane<kNTS>(a.terminated + so + blk0, (uint32_t)tid, (uint8_t)term);
+        st_lane<kNTS>(a.truncated + so + blk0, (uint32_t)tid, (uint8_t)trunc);
         if (a.info)
-            st_lane<NT>(a.info + so + blk0, (uint32_t)tid, pending ? (uint8_t)0 : (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
+            st_lane<kNTS>(a.info + so + blk0, (uint32_t)tid, pending ? (uint8_t)0 : (uint8_t)((failed ? HG_INFO_FAILED : 0) | (successed ? HG_INFO_SUCCESSED : 0) |
                                   (time_up ? HG_INFO_TIME_UP : 0) | (success_step ? HG_INFO_SUCCESS_STEP : 0) |
                                   (do_reset ? HG_INFO_RESET : 0)));
     }
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
         carry[3] = obs[16];
         if (FEAT && P.autoreset_next && done) step = -step - 1;   // reset on the next step (n = step kept)
     }
-    store_obs_wave<NT, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, a.obs, so, blk0, n, lane);
+    store_obs_wave<kNTS, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, a.obs, so, blk0, n, lane);
     }   // steps
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
     st_b = reinterpret_cast<f32x4*>(state_p + tile * kTileWords) + 4 * kTileEnvs;
@@ -566,13 +570,13 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
         // form (a 32-bit lane offset) instead of a 64-bit VALU address add per store
         uint32_t t = (uint32_t)tid;
         asm volatile("" : "+v"(t));
-        st_lane<NT>(GRP(st_b, 0), t, f32x4{hs[15], hs[16], hs[17], __int_as_float(step)});
-        st_lane<NT>(GRP(st_b, 1), t, f32x4{__int_as_float(epi), __int_as_float(succ), carry[3], carry[0]});
-        st_lane<NT>(GRP(st_b, 2), t, f32x4{carry[1], carry[2], ws[0], ws[1]});
-        st_lane<NT>(GRP(st_b, 3), t, f32x4{ws[2], ws[3], ws[4], hs[14]});
-        st_lane<NT>(GRP(st_b, 4), t, f32x4{hs[0], hs[1], hs[4], hs[5]});
-        st_lane<NT>(GRP(st_b, 5), t, f32x4{hs[6], hs[7], hs[8], hs[9]});
-        st_lane<NT>(GRP(st_b, 6), t, f32x4{hs[10], hs[11], hs[12], hs[13]});
+        st_lane<kNTS>(GRP(st_b, 0), t, f32x4{hs[15], hs[16], hs[17], __int_as_float(step)});
+        st_lane<kNTS>(GRP(st_b, 1), t, f32x4{__int_as_float(epi), __int_as_float(succ), carry[3], carry[0]});
+        st_lane<kNTS>(GRP(st_b, 2), t, f32x4{carry[1], carry[2], ws[0], ws[1]});
+        st_lane<kNTS>(GRP(st_b, 3), t, f32x4{ws[2], ws[3], ws[4], hs[14]});
+        st_lane<kNTS>(GRP(st_b, 4), t, f32x4{hs[0], hs[1], hs[4], hs[5]});
+        st_lane<kNTS>(GRP(st_b, 5), t, f32x4{hs[6], hs[7], hs[8], hs[9]});
+        st_lane<kNTS>(GRP(st_b, 6), t, f32x4{hs[10], hs[11], hs[12], hs[13]});
     }
 #undef GRP
 
@@ -1154,20 +1158,30 @@ static inline unsigned retrim_grid(int64_t jobs) {
 // size.  Until the azimuths left the stepped state, two waves per SIMD (a dynamic-LDS cap) were
 // faster past 2 M envs, where the write-heavy HBM stream binds (4 M: 271 against 284 us); with the
 // 28-word tile three are (4 M: 254.6 against 257.8 us, interleaved A/B), so the cap is gone.
-template <int T, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED>
+template <int T, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool NTS = false>
 static void launch_step(const hg_env* e, hipStream_t s, const StepArgs& a) {
     const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock);
-    hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED>), dim3(grid), dim3(kStepBlock), 0, s,
+    hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED, NTS>), dim3(grid), dim3(kStepBlock), 0, s,
                        STEP_KARGS(e), a);
 }
 
-// The step variant for a launch: NT when the batch fits one wave per SIMD; the default airframe's
-// constant-specialised kernel (baked.h) when the env uses it; with or without the optional features.
+// The step variant for a launch: NT (the lone-wave variant) while the batch fits two waves per SIMD;
+// past it the bulk variant, whose per-step launches of the default airframe store their outputs
+// non-temporally too up to four waves per SIMD (NTS: 196 608 envs 15.6 -> 14.7 us, 262 144 forward
+// flight 20.1 -> 20.0 us; from 524 288 envs on, where the outputs of one step are read back by the
+// next one through the Infinity Cache, plain stores are faster: 37.7 against 38.5 us, 1 M 67.1
+// against 69.4 us); the default airframe's constant-specialised kernel (baked.h) when the env uses
+// it; with or without the optional features.
 template <int T, bool MULTI>
 static void dispatch_step(const hg_env* e, hipStream_t s, const StepArgs& a, bool eta, bool feat) {
     auto pick = [&](auto nt) {
         constexpr bool NT = decltype(nt)::value;
         if (e->baked) {
+            if (!NT && !MULTI && e->n <= HG_NTS_WAVES * e->resident_envs) {
+                if (feat) eta ? launch_step<T, true, false, true, false, true, true>(e, s, a) : launch_step<T, false, false, true, false, true, true>(e, s, a);
+                else eta ? launch_step<T, true, false, false, false, true, true>(e, s, a) : launch_step<T, false, false, false, false, true, true>(e, s, a);
+                return;
+            }
             if (feat) eta ? launch_step<T, true, NT, true, MULTI, true>(e, s, a) : launch_step<T, false, NT, true, MULTI, true>(e, s, a);
             else eta ? launch_step<T, true, NT, false, MULTI, true>(e, s, a) : launch_step<T, false, NT, false, MULTI, true>(e, s, a);
         } else {

@@ -8,12 +8,12 @@ import re
 import shutil
 import sys
 
-# step_kernel<TASK, ETA, NT, FEAT, MULTI, BAKED>: the per-step launch of the specialised kernel
+# step_kernel<TASK, ETA, NT, FEAT, MULTI, BAKED, NTS>: the per-step launch of the specialised kernel
 # (MULTI false, BAKED true) is the judged kernel; bench.py's generic-kernel secondary figure
 # (BAKED false) and hg_rollout's multi-step launches (MULTI true) are summarised separately.
-SINGLE = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, true>")
-GENERIC = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, false>")
-MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true, (true|false)>")
+SINGLE = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, true(, (true|false))?>")
+GENERIC = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, false(, (true|false))?>")
+MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true, (true|false)(, (true|false))?>")
 
 d, tag, n, dt = sys.argv[1], sys.argv[2], int(sys.argv[3]), float(sys.argv[4])
 task = sys.argv[5] if len(sys.argv) > 5 else "hover"
