@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=1000, help="steps per timed window (exactly)")
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--repeats", type=int, default=5, help="timed windows; the median is reported")
+    ap.add_argument("--age-seconds", type=float, default=30.0,
+                    help="simulated seconds every env population is stepped (untimed, after reset) before its "
+                         "graphs are captured, so that timed windows see steady-state episode phases and resets")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--dt", type=float, default=0.01)
     ap.add_argument("--task", default="hover", choices=["hover", "forward_flight", "heli"])
@@ -258,6 +261,7 @@ class Timer:
 
     def __init__(self, torch, dist, world, dev):
         self.torch, self.dist, self.world, self.dev = torch, dist, world, dev
+        self.per_rank = None   # the last run's median window of every rank (before the max)
 
     def run(self, body, repeats, stream=None):
         t = self.torch
@@ -278,11 +282,27 @@ class Timer:
             walls.append(time.perf_counter() - w0)
             secs.append(e0.elapsed_time(e1) * 1e-3)
         v = t.tensor(secs + walls, dtype=t.float64, device=self.dev)
+        self.per_rank = [statistics.median(secs)]
         if self.world > 1:
+            mine = t.tensor([statistics.median(secs)], dtype=t.float64, device=self.dev)
+            every = [t.zeros_like(mine) for _ in range(self.world)]
+            self.dist.all_gather(every, mine)
+            self.per_rank = [float(x.item()) for x in every]
             self.dist.all_reduce(v, op=self.dist.ReduceOp.MAX)
         v = v.cpu().tolist()
         secs, walls = v[:repeats], v[repeats:]
         return statistics.median(secs), secs, statistics.median(walls)
+
+    def run_counted(self, env, body, repeats, stream=None):
+        """run(), plus the resets inside the timed windows (summed over ranks, per window)."""
+        e0 = episodes(env)
+        r = self.run(body, repeats, stream)
+        n = episodes(env) - e0
+        if self.world > 1:
+            v = self.torch.tensor([n], dtype=self.torch.int64, device=self.dev)
+            self.dist.all_reduce(v)
+            n = int(v.item())
+        return r + (n / repeats,)
 
 
 def graphs_for(torch, dev, one_step, K, B):
@@ -349,6 +369,29 @@ def action_bank(args, torch, env, n, dev, B):
         for k in range(B):
             env.random_actions(bank[k], seed=0x5EED, step=k)
     return bank
+
+
+def age(args, torch, env, bank, B, dt=None):
+    """Step a freshly reset population for --age-seconds of simulated time (untimed), so that its
+    episodes are spread over their phases -- crashes, gear contact, resets -- as in a long run.
+    Every env starts its first episode together; random-action episodes end after about 10 s
+    (SURVEY a27), so without this a short timed window right after reset holds no episode end."""
+    if args.dry_run:
+        return 0
+    steps = int(round(args.age_seconds / (dt or args.dt)))
+    for k in range(steps):
+        env.step_async(bank[k % B], with_reset_info=False)
+    torch.cuda.synchronize()
+    return steps
+
+
+def episodes(env):
+    """Episodes begun so far, summed over the envs (the episode-index counters): the difference
+    around a timed region is the number of resets inside it."""
+    if not hasattr(env, "get_state"):
+        return 0
+    _, c = env.get_state()
+    return int(c[:, 2].long().sum().item())
 
 
 def gather_loop(torch, dist, env, bank, B, K, rank, world, dev, backend, overlap=True):
@@ -452,7 +495,8 @@ def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev
         body = gather_loop(torch, dist, env5, bank5, B, K5, rank, world, dev, backend)
         body(min(args.warmup, K5))
         mode5 = mode5 or "eager, dist.gather of obs to rank 0 every step, double-buffered"
-    s_g5, _, _ = timer.run(body, R)
+    s_g5, _, _, rs_g5 = timer.run_counted(env5, body, R)
+    ranks_g5 = timer.per_rank
 
     def step5(k):
         env5.step_async(bank5[k % B], with_reset_info=False)
@@ -462,13 +506,17 @@ def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev
                 step5(k)
     else:
         rep5, _k5 = graphs_for(torch, dev, step5, K5, B)
-    s_n5, _, _ = timer.run(rep5, R)
+    s_n5, _, _, rs_n5 = timer.run_counted(env5, rep5, R)
+    ranks_n5 = timer.per_rank
     return {"workload": f"HeliHover-v0 x {CONFIG5_TOTAL} envs sharded over {world} ranks ({n5} on rank {rank})",
             "with_gather": {"value": CONFIG5_TOTAL * K5 / s_g5, "unit": "env-steps/s",
                             "ms_per_step": s_g5 / K5 * 1e3,
-                            "mode": mode5},
+                            "per_rank_ms_per_step": [x / K5 * 1e3 for x in ranks_g5],
+                            "resets_in_window": rs_g5, "mode": mode5},
             "without_gather": {"value": CONFIG5_TOTAL * K5 / s_n5, "unit": "env-steps/s",
-                               "ms_per_step": s_n5 / K5 * 1e3, "mode": f"hipGraphs of {B} steps"},
+                               "ms_per_step": s_n5 / K5 * 1e3,
+                               "per_rank_ms_per_step": [x / K5 * 1e3 for x in ranks_n5],
+                               "resets_in_window": rs_n5, "mode": f"hipGraphs of {B} steps"},
             "gather_bytes_per_step_to_rank0": (world - 1) * n5 * 17 * 4, "steps": K5}
 
 
@@ -536,6 +584,7 @@ def main():
         off, N = shard_bounds(CONFIG5_TOTAL, rank, world)
         env = make_env(args, torch, N, off, dev)
         bank = action_bank(args, torch, env, N, dev, B)
+        aged = age(args, torch, env, bank, B)
         body = None
         if backend == "nccl" and os.environ.get("HG_BENCH_CONFIG5_EAGER") != "1":
             try:
@@ -549,12 +598,14 @@ def main():
             body(min(args.warmup, K))
             if backend != "nccl" or os.environ.get("HG_BENCH_CONFIG5_EAGER") == "1":
                 mode = "eager (per-step launch + dist.gather to rank 0, double-buffered)"
-        sec, secs, wall = timer.run(body, R)
+        sec, secs, wall, resets = timer.run_counted(env, body, R)
+        per_rank = timer.per_rank
         total_envs = CONFIG5_TOTAL
     else:
         N = args.envs
         env = make_env(args, torch, N, rank * N, dev)
         bank = action_bank(args, torch, env, N, dev, B)
+        aged = age(args, torch, env, bank, B)
 
         def one_step(k):
             env.step_async(bank[k % B], with_reset_info=False)
@@ -568,7 +619,8 @@ def main():
                     one_step(k)
         else:
             replay, _keep = graphs_for(torch, dev, one_step, K, B)
-        sec, secs, wall = timer.run(replay, R)
+        sec, secs, wall, resets = timer.run_counted(env, replay, R)
+        per_rank = timer.per_rank
         mode = f"hipGraphs of {B} steps"
         total_envs = N * world
 
@@ -579,10 +631,11 @@ def main():
                 def one_step_ri(k):
                     env.step_async(bank[k % B], with_reset_info=True)
                 rep_ri, _k2 = graphs_for(torch, dev, one_step_ri, K, B)
-                s_ri, _, _ = timer.run(rep_ri, R)
+                s_ri, _, _, rs_ri = timer.run_counted(env, rep_ri, R)
                 del _k2
                 secondary["step_with_reset_info"] = {
                     "value": total_envs * K / s_ri, "unit": "env-steps/s", "ms_per_step": s_ri / K * 1e3,
+                    "resets_in_window": rs_ri,
                     "note": "step_async(with_reset_info=True): reset_index + final_obs compaction "
                             "(hg_step_chained; a memset node per captured step), hipGraph"}
                 # HeliVecEnv.step() as an RL loop calls it: eager, lazy info
@@ -592,10 +645,10 @@ def main():
                     for k in range(Ke):
                         env.step(bank[k % B])
                 eager_api()
-                s_api, s_api_all, _ = timer.run(eager_api, 5)   # median of 5 windows (host jitter)
+                s_api, s_api_all, _, rs_api = timer.run_counted(env, eager_api, 5)   # median of 5 windows (host jitter)
                 secondary["step_api_eager"] = {
                     "value": total_envs * Ke / s_api, "unit": "env-steps/s", "ms_per_step": s_api / Ke * 1e3,
-                    "steps": Ke, "windows_s": s_api_all,
+                    "steps": Ke, "windows_s": s_api_all, "resets_in_window": rs_api,
                     "note": "HeliVecEnv.step() as an RL loop calls it: eager launch of the plain "
                                          "kernel (hg_step_rows: reset envs flagged in the info bytes, their "
                                          "terminal observations at their own rows); its info dict is lazy "
@@ -604,12 +657,12 @@ def main():
                 # the generic kernel (model constants loaded, any airframe); bitwise-identical results
                 env.set_specialized(False)
                 rep_g, _k3 = graphs_for(torch, dev, one_step, K, B)
-                s_g, _, _ = timer.run(rep_g, R)
+                s_g, _, _, rs_g = timer.run_counted(env, rep_g, R)
                 del _k3
                 env.set_specialized(True)
                 secondary["generic_kernel"] = {"kernel": "generic (constants loaded, any airframe)",
                                                "value": total_envs * K / s_g, "unit": "env-steps/s",
-                                               "ms_per_step": s_g / K * 1e3}
+                                               "ms_per_step": s_g / K * 1e3, "resets_in_window": rs_g}
             if args.rollout_steps > 0 and args.reset_mode == "template":
                 Rs = args.rollout_steps
                 rbank = bank if Rs == B else torch.stack([bank[k % B] for k in range(Rs)])
@@ -619,11 +672,11 @@ def main():
                 def rollouts():
                     for _ in range(nroll):
                         env.rollout(rbank, out=rout)
-                s_r, _, _ = timer.run(rollouts, R)
+                s_r, _, _, rs_r = timer.run_counted(env, rollouts, R)
                 secondary["rollout"] = {
                     "api": "hg_rollout", "steps_per_launch": Rs, "steps": nroll * Rs,
                     "value": total_envs * nroll * Rs / s_r, "unit": "env-steps/s",
-                    "ms_per_step": s_r / (nroll * Rs) * 1e3,
+                    "ms_per_step": s_r / (nroll * Rs) * 1e3, "resets_in_window": rs_r,
                     "bytes_per_env_step": ROLLOUT_BYTES_PER_ENV_STEP + BYTES_STATE_RW / Rs,
                     "note": "open-loop action sequences (planning / data generation); same results as "
                             "hg_step, state read and written once per launch"}
@@ -636,13 +689,17 @@ def main():
 
             def stepr(k):
                 envr.step_async(bank[k % B], with_reset_info=False)
+            aged_r = age(args, torch, envr, bank, B)
             for k in range(min(args.warmup, 50)):
                 stepr(k)
             repr_, _kr = graphs_for(torch, dev, stepr, Kr, B)
-            s_rt, _, _ = timer.run(repr_, 3)
+            s_rt, _, _, rs_rt = timer.run_counted(envr, repr_, 3)
             del _kr
+            # a window without a reset would time the plain step, not the re-trim: no value then
             secondary["retrim"] = {
-                "envs": N, "value": N * Kr / s_rt, "unit": "env-steps/s", "ms_per_step": s_rt / Kr * 1e3,
+                "envs": N, "value": N * Kr / s_rt if rs_rt > 0 else None, "unit": "env-steps/s",
+                "ms_per_step": s_rt / Kr * 1e3 if rs_rt > 0 else None, "window_ms_per_step": s_rt / Kr * 1e3,
+                "resets_in_window": rs_rt, "aged_steps": aged_r,
                 "steps": Kr, "retrim_failures": envr.retrim_failures(),
                 "note": "reset_mode='retrim': each step's auto-resets re-trimmed on the device (Newton trim "
                         "against the env's last wind, the reference's reset from episode 2 on), hipGraph"}
@@ -658,15 +715,17 @@ def main():
 
             def stepx(k):
                 envx.step_async(bankx[k % B], with_reset_info=False)
+            aged_x = age(args, torch, envx, bankx, B)
             for k in range(min(args.warmup, 20)):
                 stepx(k)
             repx, _kx = graphs_for(torch, dev, stepx, Kx, B)
-            s_x, _, _ = timer.run(repx, 3)
+            s_x, _, _, rs_x = timer.run_counted(envx, repx, 3)
             del _kx
             ach = Nx * BYTES_PER_ENV_STEP / (s_x / Kx) / 1e9
             secondary["out_of_cache"] = {
                 "envs": Nx, "value": Nx * Kx / s_x, "unit": "env-steps/s", "ms_per_step": s_x / Kx * 1e3,
                 "steps": Kx, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
+                "resets_in_window": rs_x, "aged_steps": aged_x,
                 "traffic": (pmc_traffic(Nx, args.dt, args.task) or (None,))[0],
                 "traffic_source": (pmc_traffic(Nx, args.dt, args.task) or (None, None))[1],
                 "note": "working set 1.32 GB per launch, past the 256 MB MALL: the traffic is HBM bytes"}
@@ -683,6 +742,7 @@ def main():
             try:
                 env5 = make_env(args, torch, n5, off5, dev)
                 bank5 = action_bank(args, torch, env5, n5, dev, B)
+                age(args, torch, env5, bank5, B)
             except Exception as e:   # e.g. out of memory on one rank
                 ok, err5 = 0, repr(e)
             flag = torch.tensor([ok], dtype=torch.int32, device=dev)
@@ -728,7 +788,11 @@ def main():
                    "parallelism": f"env-shard x{world}", "world_size_seen": seen_world,
                    "backend": backend or "none (1 rank)"},
         "timing": {"repeats": R, "window_s": secs, "median_window_s": sec, "wall_median_s": wall,
-                   "steps_per_window": K},
+                   "steps_per_window": K, "aged_steps": aged,
+                   "aged_note": f"each env population stepped {args.age_seconds:g} simulated s (untimed) after reset "
+                                "before capture: windows see steady-state episode phases",
+                   "resets_in_window": resets,
+                   "per_rank_ms_per_step": [x / K * 1e3 for x in per_rank]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": f"step_kernel<{args.task.upper()}>", "kernel_avg_us": kern_s * 1e6,

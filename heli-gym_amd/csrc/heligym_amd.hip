@@ -685,8 +685,10 @@ __global__ __launch_bounds__(kBlock) void init_kernel(const Template<float> T, f
 }
 
 // tiles -> [N, 27] state / [N, 3] counter records (get_state); the azimuths reconstructed, the step
-// counter of an env waiting for its next-step reset exported as -1
-__global__ __launch_bounds__(kBlock) void get_rows_kernel(const uint32_t* tiles, const AzRec* az,
+// counter of an env waiting for its next-step reset exported as -1.  The reconstruction replays one
+// add-and-wrap per step since the record's anchor, so the record is re-anchored at the values it
+// returns: a later read replays only the steps taken since this one (bitwise the same values)
+__global__ __launch_bounds__(kBlock) void get_rows_kernel(const uint32_t* tiles, AzRec* az,
                                                           const Template<float>* T, const float* tmpl_env,
                                                           const Params<float>* P, uint32_t* state_rows,
                                                           int32_t* counter_rows, int64_t n) {
@@ -701,6 +703,7 @@ __global__ __launch_bounds__(kBlock) void get_rows_kernel(const uint32_t* tiles,
         const float2 a = az_now(az[i], step, epi, ta[0], ta[1], P->f_dpsi_mr, P->f_dpsi_tr);
         state_rows[i * kStateCols + hgk::kAzCol0] = __float_as_uint(a.x);
         state_rows[i * kStateCols + hgk::kAzCol0 + 1] = __float_as_uint(a.y);
+        az[i] = AzRec{a.x, a.y, hgk::episode_steps(step), epi};
     }
     if (counter_rows) {
         counter_rows[i * kCtrCols + 0] = step < 0 ? -1 : step;
@@ -1606,8 +1609,12 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     a.tmpl_env = e->tmpl_env;
     a.nsteps = nsteps;
     a.retrim_slot = -1;
+    // reset_mode RETRIM without auto-reset: every step records its wind, the trim wind of a later
+    // hg_reset (helicopter.py:208-212), as K hg_step calls would
+    a.retrim_wind = e->retrim_wind;
     hipStream_t s = (hipStream_t)stream;
-    const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
+    const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates ||
+                      e->Pf.reset_retrim;
     dispatch_task<true>(e, s, a, eta != nullptr, feat);
     HIP_TRY(hipGetLastError());
     return HG_OK;

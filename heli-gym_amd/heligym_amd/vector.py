@@ -454,7 +454,12 @@ class HeliVecEnv(*_VEC_BASES):
 
     # ------------------------------------------------------------------ state access
     def get_state(self):
-        """(state [N,27] float32, counters [N,3] int32): heli 18 | wind 5 | carry 4."""
+        """(state [N,27] float32, counters [N,3] int32): heli 18 | wind 5 | carry 4.
+
+        The rotor azimuths (columns 2, 3) are reconstructed from a per-env record (each step adds
+        dt * Omega and wraps, bitwise what the step would have carried); the cost is one add-and-wrap
+        per step since the env's last reset, set_state or get_state, and each call re-anchors the
+        records, so a run that reads its state now and then keeps every read short."""
         t = self.torch
         s = t.empty((self.num_envs, _abi.HG_STATE_COLS), dtype=t.float32, device=self.device)
         c = t.empty((self.num_envs, _abi.HG_COUNTER_COLS), dtype=t.int32, device=self.device)

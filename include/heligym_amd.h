@@ -288,7 +288,8 @@ int32_t hg_retrim_failures(hg_env* env, int64_t* count);
  * counters [N,HG_COUNTER_COLS] i32 (either may be NULL).  The rotor azimuths (state columns 2, 3)
  * are not part of the stepped state: hg_get_state reconstructs them (each step adds dt * Omega and
  * wraps, bitwise what the step would have carried), at a cost linear in the steps since the env's
- * last reset / set_state.  A negative episode-step counter marks an env whose next-step auto-reset
+ * last reset / set_state / hg_get_state (each read re-anchors the env's azimuth record at the values
+ * it returns, so periodic reads keep every read short).  A negative episode-step counter marks an env whose next-step auto-reset
  * is due (read back as -1). */
 int32_t hg_get_state(hg_env* env, float* state_dev, int32_t* counters_dev, void* stream);
 int32_t hg_set_state(hg_env* env, const float* state_dev, const int32_t* counters_dev, void* stream);

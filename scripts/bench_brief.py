@@ -1,0 +1,15 @@
+"""One line per bench JSON file: the headline and every secondary's ms/step and resets in window."""
+import json
+import sys
+
+for f in sys.argv[1:]:
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    t = d.get("timing", {})
+    out = [f"{f}: K={d['steps']} head {d['ms_per_step'] * 1e3:.3f} us (resets/window {t.get('resets_in_window')}, "
+           f"aged {t.get('aged_steps')}) frac {d['roofline']['frac']:.3f}"]
+    for k in ("step_with_reset_info", "step_api_eager", "generic_kernel", "rollout", "retrim", "out_of_cache"):
+        v = d.get(k)
+        if v:
+            ms = v.get("ms_per_step") if v.get("ms_per_step") is not None else v.get("window_ms_per_step")
+            out.append(f"  {k}: {ms * 1e3 if ms else float('nan'):.2f} us resets {v.get('resets_in_window')}")
+    print("\n".join(out))

@@ -68,12 +68,18 @@ def test_reanchored_twin_is_bitwise_identical(torch, mode):
     B.close()
 
 
-def test_azimuths_advance_and_reset_to_template(torch):
+@pytest.mark.parametrize("reset_mode,mode", [("template", "same_step"), ("retrim", "same_step"),
+                                             ("retrim", "next_step")])
+def test_azimuths_advance_and_reset_to_template(torch, reset_mode, mode):
     """Each step adds f_dpsi = dt * Omega to both azimuths and wraps them; a reset puts the
     template's azimuths back; a changed trim condition re-anchors the running episodes (no jump)
-    and later resets start from the new template."""
+    and later resets start from the new template.  In reset_mode "retrim" the reset state comes
+    from the device trim (retrim_write writes the azimuth record), under both auto-reset modes
+    (next_step: an env that ended at step k resets at step k + 1), with trim azimuths that are not
+    the defaults."""
     N, K = 2048, 400
-    env = _env(N, autoreset=True)
+    env = _env(N, autoreset=True, reset_mode=reset_mode, autoreset_mode=mode,
+               trim_cond={"psi_mr": 0.5, "psi_tr": 2.5})
     env.reset()
     om = np.array([env.cfg.af.mr_RPM, env.cfg.af.tr_RPM], np.float64) * 2 * np.pi / 60
     d = om * env.dt
@@ -83,6 +89,7 @@ def test_azimuths_advance_and_reset_to_template(torch):
     prev = s[:, 2:4].cpu().numpy()
     np.testing.assert_array_equal(prev, np.tile(tmpl, (N, 1)))
     changed, resets = False, 0
+    pending = np.zeros(N, bool)   # next_step: ended last step, resets this step
     for k in range(K):
         if k == K // 2:   # new template azimuths mid-run
             before = env.get_state()[0][:, 2:4].cpu().numpy()
@@ -95,16 +102,20 @@ def test_azimuths_advance_and_reset_to_template(torch):
         env.random_actions(act, seed=9, step=k)
         act[::2, 0] = -1.0   # crashes on every other env, after the template change
         _, _, term, trunc, _ = env.step(act)
-        done = (term | trunc).cpu().numpy()
+        ended = (term | trunc).cpu().numpy()
+        reset_now = ended if mode == "same_step" else pending
         cur = env.get_state()[0][:, 2:4].cpu().numpy()
         assert np.all(cur >= -np.float32(np.pi)) and np.all(cur < np.float32(np.pi))
-        np.testing.assert_array_equal(cur[done], np.tile(tmpl, (int(done.sum()), 1)))
-        live = ~done
+        np.testing.assert_array_equal(cur[reset_now], np.tile(tmpl, (int(reset_now.sum()), 1)))
+        live = ~reset_now
         ok = _ang_close(cur[live], prev[live] + d)
         assert ok.all(), (k, np.argwhere(~ok)[:3])
         prev = cur
-        resets += int(done.sum())
+        resets += int(reset_now.sum())
+        pending = ended & ~reset_now if mode == "next_step" else pending
     assert changed and resets > N // 4, resets
+    if reset_mode == "retrim":
+        assert env.retrim_failures() == 0
     env.close()
 
 

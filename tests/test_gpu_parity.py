@@ -894,6 +894,43 @@ def test_rollout_equals_sequential_steps(torch, opts):
         np.testing.assert_array_equal(x, y)
 
 
+@pytest.mark.parametrize("max_steps", [None, 37])
+def test_rollout_retrim_without_autoreset_then_reset(torch, max_steps):
+    """reset_mode="retrim" with auto-reset off: a rollout records each step's wind like K step()
+    calls, so the reset() after it re-trims against the same last wind (F8, helicopter.py:208-212);
+    with a TimeLimit the feature kernel runs (its wind store must see the buffer)."""
+    N, K = 300, 60
+    outs = []
+    for mode in ("steps", "rollout"):
+        env = make_env(torch, N, "hover", 0.02, autoreset=False, seed=5, reset_mode="retrim",
+                       max_episode_steps=max_steps)
+        env.reset()
+        acts = torch.empty((K, N, 4), dtype=torch.float32, device=env.device)
+        for k in range(K):
+            env.random_actions(acts[k], seed=9, step=k)
+        if mode == "steps":
+            rec = [[] for _ in range(4)]
+            for k in range(K):
+                env.step_async(acts[k], with_reset_info=False)
+                for lst, buf in zip(rec, (env.obs, env.reward, env.terminated_u8, env.truncated_u8)):
+                    lst.append(buf.clone())
+            res = [torch.stack(r) for r in rec]
+        else:
+            res = list(env.rollout(acts))[:4]
+        pre, _ = env.get_state()
+        obs0, _ = env.reset()
+        st, ctr = env.get_state()
+        torch.cuda.synchronize()
+        assert env.retrim_failures() == 0
+        outs.append([r.cpu().numpy() for r in res] + [pre.cpu().numpy(), obs0.cpu().numpy(), st.cpu().numpy(),
+                                                      ctr.cpu().numpy()])
+        env.close()
+    for x, y in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(x, y)
+    # the re-trimmed resets differ from the mean-wind template (the winds were turbulent)
+    assert np.abs(outs[0][-2][:, 6:9] - outs[0][-2][:1, 6:9]).max() > 0
+
+
 def _random_conds(rng, k):
     # hover-to-cruise starts: the trim's Newton path (stopped at ||y - y*||^2 <= 1e-4) is sensitive
     # to last-ulp differences of the fp64 transcendentals (ocml vs glibc) only for extreme mixes

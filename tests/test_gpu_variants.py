@@ -37,11 +37,15 @@ def _run(torch, n, offset, K):
 
 
 def test_nt_variant_equals_bulk_variant(torch):
-    """One batch of 2 x 99 000 envs (bulk variant, three waves per SIMD) against its two halves
-    stepped as batches of 99 000 (NT variant, two waves per SIMD; ragged last wave): every
-    observation, reward and done flag and the final state bitwise equal, resets included.
-    (The threshold depends on the CU count; on MI355X's 256 CUs the NT range ends at 131 072.)"""
-    H, K = 99_000, 350
+    """One batch of 2 H envs (bulk variant, past two waves per SIMD) against its two halves stepped
+    as batches of H (NT variant, at most two waves per SIMD; ragged last wave): every observation,
+    reward and done flag and the final state bitwise equal, resets included.  The NT range ends at
+    2 waves x 64 lanes x 4 SIMDs x CUs envs (131 072 on MI355X's 256 CUs); H is sized from the
+    device's CU count so that H is inside it and 2 H past it on any device."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    nt_max = 2 * 64 * 4 * cus
+    H, K = (3 * nt_max) // 4 + 7, 350
+    assert H <= nt_max < 2 * H
     full = _run(torch, 2 * H, 0, K)
     lo = _run(torch, H, 0, K)
     hi = _run(torch, H, H, K)
