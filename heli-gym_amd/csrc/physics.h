@@ -49,7 +49,47 @@ HD void m_sincos(float x, float* s, float* c) {
     *s = (q & 2) ? -ss : ss;
     *c = ((q + 1) & 2) ? -cc : cc;
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// fp64 on the device (the re-trim kernel, retrim.hip): sin and cos from one reduction -- Cody-Waite
+// by pi/2 with fused multiply-adds (3-part constant, exact enough for |x| < 1e5; trim attitudes are
+// below pi) and the fdlibm kernel polynomials __kernel_sin / __kernel_cos on [-pi/4, pi/4] (about
+// 1 ulp, like the host's libm, which the trims do not reproduce bitwise either) -- instead of two
+// library calls with separate reductions and a Payne-Hanek path each.
+HD void m_sincos(double x, double* s, double* c) {
+    const double k = rint(x * 0.63661977236758134308);
+    double r = fma(k, -1.57079632679489655800e+00, x);
+    r = fma(k, -6.12323399573676603587e-17, r);
+    r = fma(k, 1.49738490485916983e-33, r);
+    const double z = r * r, v = z * r;
+    const double sp = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10, -2.50507602534068634195e-08),
+                                        2.75573137070700676789e-06), -1.98412698298579493134e-04),
+                          8.33333333332248946124e-03);
+    const double sr = fma(v, fma(z, sp, -1.66666666666666324348e-01), r);
+    const double cp = z * fma(z, fma(z, fma(z, fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                                                  -2.75573143513906633035e-07), 2.48015872894767294178e-05),
+                                     -1.38888888888741095749e-03), 4.16666666666666019037e-02);
+    const double hz = 0.5 * z, w = 1.0 - hz;
+    const double cr = w + (((1.0 - w) - hz) + z * cp);
+    const int q = (int)k;
+    const double ss = (q & 1) ? cr : sr, cc = (q & 1) ? sr : cr;
+    *s = (q & 2) ? -ss : ss;
+    *c = ((q + 1) & 2) ? -cc : cc;
+}
+#else
 HD void m_sincos(double x, double* s, double* c) { *s = sin(x); *c = cos(x); }
+#endif
+// x / c for a model constant c with its reciprocal ic = 1 / c: on the device one product and a
+// fused-multiply-add correction (the quotient to within an ulp, no division sequence); the host
+// divides.
+HD double m_div_c(double x, double c, double ic) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double q = x * ic;
+    return fma(fma(-q, c, x), ic, q);
+#else
+    (void)ic;
+    return x / c;
+#endif
+}
 
 // sin/cos of the three attitude angles (kinematic.py:4-5,21-22).
 template <typename R>

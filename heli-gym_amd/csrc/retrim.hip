@@ -1,11 +1,15 @@
 // retrim.hip — the device batched Newton trim: exact second-episode resets (reset_mode RETRIM,
 // SURVEY F8), hg_trim_batch and hg_trim_conds_batch.
 //
-// Its own translation unit, compiled with -ffp-contract=off: the reference's trim is numpy without
-// fused multiply-adds and its stopping point depends on the Newton path (an ill-conditioned
-// system stopped at ||y - y*||^2 <= 1e-4), so the device evaluates exactly the host's operation
-// sequence (heligym_amd.hip::do_trim, which reproduces the reference's trims) instead of a fused
-// one whose different roundings can change a line-search decision.
+// HelicopterDynamics.trim (helicopter_dynamics.py:491-555) for many winds at once, one wave per trim,
+// fp64 throughout: the reference's Newton iteration (central-difference Jacobian, step halving,
+// stop at ||y - y*||^2 <= 1e-4) with its 42 model evaluations per round spread over the lanes and
+// the 16 x 16 solve one row per lane.  Its own translation unit, built with -ffp-contract=fast: the
+// device evaluates the model with fused multiply-adds, one-reduction sin/cos and reciprocal
+// divisions by model constants (physics.h device overloads), a few-ulp rounding of the same fp64
+// arithmetic.  The host's serial trim (heligym_amd.hip::do_trim) is not reproduced bitwise (its
+// libm transcendentals differ from any device library anyway); the tests hold the device trims to
+// it and to the reference's recorded resets at fp32 resolution.
 #include "../../include/heligym_amd.h"
 #include "retrim.h"
 
@@ -14,9 +18,6 @@ namespace {
 
 #ifndef HG_TIMING
 #define HG_TIMING 0
-#endif
-#ifndef HG_GJ_FLOW   // Gauss-Jordan pivot steps without per-step early exits (see gj_step)
-#define HG_GJ_FLOW 1
 #endif
 #if HG_TIMING
 // diagnostic build: s_memtime at the phase boundaries of the first job's rounds (lane 0)
@@ -27,29 +28,9 @@ __device__ unsigned long long g_rt_timing[64];
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();                   \
         if (l == 0 && job == 0 && (j) < 64) g_rt_timing[(j)] = t_;                    \
     } while (0)
-// sub-phases of the first two pivot steps of one solve (slots 40..51)
-#define GJSTAMP(j, ...)                                                               \
-    do {                                                                              \
-        if (stamp && c < 2) {                                                         \
-            asm volatile("" ::__VA_ARGS__);                                           \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();               \
-            if (l == 0) g_rt_timing[40 + 6 * c + (j)] = t_;                           \
-        }                                                                             \
-    } while (0)
 #else
 #define RSTAMP(j, ...) do { } while (0)
-#define GJSTAMP(j, ...) do { } while (0)
 #endif
-
-// HelicopterDynamics.trim (helicopter_dynamics.py:491-555) for many winds at once: the reset path of
-// reset_mode RETRIM (F8) and hg_trim_batch.  One wave per trim, fp64 throughout, every lane holding
-// the same Newton iterate:
-//   * lanes 0..15 / 16..31 evaluate the +eps / -eps Jacobian columns in parallel;
-//   * the Gauss-Jordan elimination of [J | r] (hg::solve16, same operation order) runs over the
-//     whole wave, four lanes per row (gauss_jordan_wave);
-//   * lanes 0..9 evaluate the ten step-halving trials at once; the first one that lowers the
-//     residual is the trial the reference's sequential search accepts.
-
 
 __device__ __forceinline__ double read_lane(double v, int lane) {
     const uint64_t u = __double_as_longlong(v);
@@ -57,155 +38,119 @@ __device__ __forceinline__ double read_lane(double v, int lane) {
     const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
-__device__ __forceinline__ double shfl_d(double v, int src) {
-    const uint64_t u = __double_as_longlong(v);
-    const uint32_t lo = __shfl((int)(uint32_t)u, src);
-    const uint32_t hi = __shfl((int)(uint32_t)(u >> 32), src);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
 
-// hg::solve16 (np.linalg.inv(dydx) @ r, helicopter_dynamics.py:524-527): Gauss-Jordan with partial
-// pivoting on the augmented matrix [J | r] spread over the whole wave.  Lane l = 16 q + i holds row i
-// of columns 4q .. 4q+3 and of the right-hand side (a[0..3], a[4]; the right-hand side is kept by all
-// four lanes of a row, which compute it identically), so a DPP row of 16 lanes is one column
-// quarter.  Per pivot step C:
-//   * the pivot search is a 4-level DPP rotation max over the 16 rows of column C (in the row of
-//     lanes that holds it) instead of a serial scan, and a ballot of the rows attaining it;
-//   * rows are never moved: every row carries its position in the host's row order (`pos`, the
-//     same in its four lanes), exchanged by the pivot step as the host exchanges the rows, and the
-//     search breaks ties by that position, so the pivot is the host's (first row of maximal |M[i][C]|
-//     among positions C..15, strict >);
-//   * the multiplier M[i][C] (from the lane of this row that holds column C) and the pivot row's
-//     elements (from the lane of the pivot row that holds this lane's columns) are two ds_bpermute
-//     reads; the first is issued before the search, as it does not depend on the pivot;
-//   * each lane scales the pivot row by 1/pivot and eliminates its own five elements.
-// The values of columns >= C and of the right-hand side are the host's bit for bit (hg::solve16 in
-// the same operation order, unfused); columns < C, which the host leaves alone and never reads
-// again, are updated here too and ignored.  The solution is the right-hand side in host order.
-// The block is one wave, whose LDS operations execute in issue order: a read issued after a write
-// sees it.  This only keeps the compiler from reordering LDS accesses across the point (no
-// s_barrier, no wait for the LDS queue to drain).
+// The wave is the block: its LDS operations execute in issue order, so a read issued after a write
+// sees it.  This only keeps the compiler from reordering LDS accesses across the point.
 __device__ __forceinline__ void lds_order() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
 }
 
-// Rotate a double within each row of 16 lanes (DPP row_ror: every lane has a source, so no
-// "old" operand is needed); n is a compile-time constant after inlining.
-__device__ __forceinline__ double ror16_d(double v, int n) {
-    const uint64_t u = __double_as_longlong(v);
-    int lo = (int)(uint32_t)u, hi = (int)(uint32_t)(u >> 32);
-    switch (n) {
-        case 8: lo = __builtin_amdgcn_mov_dpp(lo, 0x128, 0xF, 0xF, true); hi = __builtin_amdgcn_mov_dpp(hi, 0x128, 0xF, 0xF, true); break;
-        case 4: lo = __builtin_amdgcn_mov_dpp(lo, 0x124, 0xF, 0xF, true); hi = __builtin_amdgcn_mov_dpp(hi, 0x124, 0xF, 0xF, true); break;
-        case 2: lo = __builtin_amdgcn_mov_dpp(lo, 0x122, 0xF, 0xF, true); hi = __builtin_amdgcn_mov_dpp(hi, 0x122, 0xF, 0xF, true); break;
-        default: lo = __builtin_amdgcn_mov_dpp(lo, 0x121, 0xF, 0xF, true); hi = __builtin_amdgcn_mov_dpp(hi, 0x121, 0xF, 0xF, true); break;
-    }
-    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
-}
-// v_max_f64 without the canonicalising maxes fmax() adds (the operands here are never NaN)
-__device__ __forceinline__ double vmax_d(double a, double b) {
-    double r;
-    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
+// 1 / x for a finite non-zero x: v_rcp_f64 and two Newton steps (fused), within an ulp
+__device__ __forceinline__ double rcp_f64(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
 }
 
+// max of a 32-bit key over each row of 16 lanes (DPP row rotations; every lane has a source)
+__device__ __forceinline__ uint32_t row16_max(uint32_t k) {
+    k = max(k, (uint32_t)__builtin_amdgcn_mov_dpp((int)k, 0x128, 0xF, 0xF, true));
+    k = max(k, (uint32_t)__builtin_amdgcn_mov_dpp((int)k, 0x124, 0xF, 0xF, true));
+    k = max(k, (uint32_t)__builtin_amdgcn_mov_dpp((int)k, 0x122, 0xF, 0xF, true));
+    k = max(k, (uint32_t)__builtin_amdgcn_mov_dpp((int)k, 0x121, 0xF, 0xF, true));
+    return k;
+}
+
+// np.linalg.inv(dydx) @ r (helicopter_dynamics.py:524-527) as Gauss-Jordan with partial pivoting,
+// one row per lane: lane l holds row i = l & 15 of [J | r] (the four rows of 16 lanes are identical
+// copies).  Per pivot step C (unrolled, so every column index is a register):
+//   * the pivot is the unused row with the largest |J[i][C]|, found with a DPP max over the 16 rows
+//     on the high word of |J[i][C]| (monotonic in |x|; rows within 2^-20 of the maximum tie and the
+//     lowest row wins: any of them is as good a pivot, partial pivoting only needs a large one);
+//   * the pivot row is read with readlanes (its row index is uniform), each row subtracts
+//     (J[i][C] / pivot) x the pivot row with one fused multiply-add per element, and the pivot row
+//     is scaled by 1 / pivot;
+//   * rows never move: each remembers the column it was the pivot of, and the solution is the
+//     right-hand side in that order.
+// Columns < C are neither read nor updated after step C (the host's solve16 updates them and never
+// reads them again).  Fused arithmetic and a different tie rule make this a different rounding of
+// the same solve (the trims are compared with the host's to fp32 resolution, not bitwise).
 template <int C>
-__device__ __forceinline__ bool gj_step(double (&a)[5], int& pos, int l, bool stamp) {
-    constexpr int c = C, qc = C >> 2, tc = C & 3;
-    (void)stamp;
-    (void)c;
-    const int i = l & 15, q = l >> 4;
-    GJSTAMP(0, "v"(a[0]));
-    const double f = shfl_d(a[tc], 16 * qc + i);   // M[i][C] of this lane's row
-    const double v = a[tc];                         // M[i][4q + tc]; row of lanes qc: column C
-    const bool nan_v = v != v;
-    const bool cand = pos >= C && !nan_v;
-    const double key = cand ? fabs(v) : -1.0;
-    double mx = key;                                // max |M[i][C]| over the candidate rows
+__device__ __forceinline__ void gj_step(double (&A)[16], double& b, bool& used, int& mycol, bool& bad, int i) {
+    const double v = A[C];
+    const uint32_t hi = (uint32_t)(__double_as_longlong(v) >> 32) & 0x7FFFFFFFu;
+    const uint32_t key = used ? 0u : hi;
+    const uint32_t mx = row16_max(key);
+    const uint32_t hit = (uint32_t)__ballot(key == mx) & 0xFFFFu;   // rows of the first 16 lanes
+    const int P = __builtin_ctz(hit | 0x10000u);
+    const double mp = read_lane(v, P);
+    bad = bad || mx == 0u || !isfinite(mp);
+    const double rinv = rcp_f64(mp);
+    const bool piv = i == P;
+    // other rows: A - (v / pivot) pj; the pivot row: A / pivot -- one form for both, A * m - g pj with
+    // (m, g) = (1, v / pivot) or (1 / pivot, 0): the product by 1 and the fused add of -0 are exact
+    const double g = piv ? 0.0 : v * rinv;
+    const double m = piv ? rinv : 1.0;
 #pragma unroll
-    for (int sh = 8; sh >= 1; sh >>= 1) mx = vmax_d(mx, ror16_d(mx, sh));
-    // the rows that attain it (usually one); ties go to the smallest host position
-    const uint32_t hit = (uint32_t)(__ballot(cand && key == mx) >> (16 * qc)) & 0xFFFFu;
-    int P = hit ? __builtin_ctz(hit) : 0;
-    int ppos = __builtin_amdgcn_readlane(pos, 16 * qc + P);
-    if (hit & (hit - 1)) {   // wave-uniform, rare
-        for (uint32_t m = hit & (hit - 1); m; m &= m - 1) {
-            const int b = __builtin_ctz(m);
-            const int pb = __builtin_amdgcn_readlane(pos, 16 * qc + b);
-            if (pb < ppos) { ppos = pb; P = b; }
-        }
-    }
-    const double mp = read_lane(v, 16 * qc + P);    // the pivot M[P][C]
-    double pr[5];
-#pragma unroll
-    for (int t = 0; t < 5; ++t) pr[t] = shfl_d(a[t], 16 * q + P);   // the pivot row
-    // the host's first candidate M[C][C] being NaN keeps it as the (non-finite) pivot
-    const bool c_nan = __ballot(q == qc && pos == C && nan_v) != 0;
-    GJSTAMP(1, "s"(P));
-    const bool bad = !hit || c_nan || mp == 0.0 || !isfinite(mp);
-#if HG_GJ_FLOW
-    // No branch on a failed pivot step: it is reported after the last step (the steps in between
-    // compute values nobody reads), so a step's remaining eliminations and the next step's pivot
-    // search share a basic block and the scheduler overlaps them.
-#else
-    if (bad) return false;
-    __builtin_amdgcn_sched_barrier(0);   // the pivot-row reads are in flight during the division
-#endif
-    const double rinv = 1.0 / mp;
-#pragma unroll
-    for (int t = 0; t < 5; ++t) pr[t] *= rinv;
-    GJSTAMP(2, "v"(pr[0]), "v"(pr[4]));
-    const bool is_piv = i == P;
-#pragma unroll
-    for (int t = 0; t < 5; ++t) {
-        const double u = a[t] - f * pr[t];
-        a[t] = is_piv ? pr[t] : (f != 0.0 ? u : a[t]);
-    }
-    pos = pos == ppos ? C : (pos == C ? ppos : pos);
-    GJSTAMP(3, "v"(a[0]), "v"(a[4]));
-    return !bad;
+    for (int j = C + 1; j < 16; ++j) A[j] = fma(-g, read_lane(A[j], P), A[j] * m);
+    b = fma(-g, read_lane(b, P), b * m);
+    used = used || piv;
+    mycol = piv ? C : mycol;
 }
 template <int C>
-__device__ __forceinline__ bool gj_steps(double (&a)[5], int& pos, int l, bool stamp) {
-#if HG_GJ_FLOW
-    const bool ok = gj_step<C>(a, pos, l, stamp);
-    if constexpr (C < 15) {
-        const bool rest = gj_steps<C + 1>(a, pos, l, stamp);
-        return ok && rest;
+__device__ __forceinline__ void gj_steps(double (&A)[16], double& b, bool& used, int& mycol, bool& bad, int i) {
+    gj_step<C>(A, b, used, mycol, bad, i);
+    if constexpr (C < 15) gj_steps<C + 1>(A, b, used, mycol, bad, i);
+}
+
+// What the observation needs from one evaluation beyond the state: power, uvw_air, ned velocity
+// (observe(), helicopter_dynamics.py:471-488).
+struct EvalExt {
+    double o[7];
+};
+
+// __trim_fcn (helicopter_dynamics.py:557-576, trim.h trim_fcn): the normalised derivatives y(x) at
+// one trial point, and the observation's non-state terms.
+__device__ __forceinline__ void trim_eval(const hg::Params<double>& P, const hg::TrimSetup& T, const double x[16],
+                                          const double W[3], double y[16], EvalExt& e) {
+    double s[18], d[18];
+    hg::trim_state(P, T.base, x, s);
+    const hg::Controls<double> u = hg::controls(P, x[12], x[13], x[14], x[15]);
+    hg::Attitude<double> att;
+    hg::m_sincos(s[12], &att.s[0], &att.c[0]);
+    hg::m_sincos(s[13], &att.s[1], &att.c[1]);
+    att.s[2] = T.s_psi;
+    att.c[2] = T.c_psi;
+    const hg::Frame<double> f = hg::frame(P, s, W, T.hc, att, T.rho_irho);
+    const hg::Loads<double> A = hg::main_loads(P, s, u, f);
+    const hg::Loads<double> B = hg::tail_loads(P, s, u, f);
+    hg::eom(P, s, f, A, B, d);
+    y[0] = hg::m_div_c(d[0], P.mr_VTIP, P.mr_inv_VTIP);
+    y[1] = hg::m_div_c(d[1], P.tr_VTIP, P.tr_inv_VTIP);
+    y[2] = d[4];
+    y[3] = d[5];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        y[4 + k] = hg::m_div_c(d[6 + k], P.mr_VTIP, P.mr_inv_VTIP);
+        y[7 + k] = hg::m_div_c(d[9 + k], P.mr_OMEGA, P.mr_inv_OMEGA);
+        y[10 + k] = d[12 + k];
+        y[13 + k] = hg::m_div_c(d[15 + k], P.mr_R, P.mr_inv_R);
     }
-    return ok;
-#else
-    if (!gj_step<C>(a, pos, l, stamp)) return false;
-    if constexpr (C < 15) return gj_steps<C + 1>(a, pos, l, stamp);
-    return true;
-#endif
+    e.o[0] = ((A.power + B.power) + P.p_loss) * (1.0 / 550.0);
+    e.o[1] = f.ua; e.o[2] = f.va; e.o[3] = f.wa;
+    e.o[4] = f.n0; e.o[5] = f.n1; e.o[6] = f.n2;
 }
 
-// The Newton system arrives in LDS as the raw evaluations: E[j][k] = y_k at x + eps e_j (j < 16) and
-// at x - eps e_{j-16} (16 <= j < 32), R[k] = y_k - y*_k.  Each lane forms its own four Jacobian
-// elements (J[i][j] = (E[j][i] - E[j+16][i]) / (2 eps), helicopter_dynamics.py:521-523, the host's
-// operation) and right-hand side, so the 256 divisions are spread over the wave (4 per lane); the
-// solution leaves through `sol` in host row order.
-__device__ __forceinline__ bool gauss_jordan_wave(const double* E, const double* R, double* sol, int l, bool stamp,
-                                                  double (&dir)[16]) {
-    const int i = l & 15, q = l >> 4;
-    const double eps = hg::kTrimEps;
-    double a[5];
+__device__ __forceinline__ void retrim_write(const RetrimArgs& a, const hg::Params<double>& P, const hg::TrimSetup& T,
+                                             int64_t job, int64_t env, const double x[16], const double* ext) {
+    double s[18], ob[17];
+    hg::trim_state(P, T.base, x, s);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) a[t] = (E[(4 * q + t) * 16 + i] - E[(4 * q + t + 16) * 16 + i]) / (2 * eps);
-    a[4] = R[i];
-    int pos = i;
-    if (!gj_steps<0>(a, pos, l, stamp)) return false;
-    if (l < 16) sol[pos] = a[4];
-    lds_order();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) dir[k] = sol[k];
-    return true;
-}
-
-__device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, int64_t env, const double x[16],
-                                             const double s[18], const double ob[17]) {
+    for (int c = 0; c < 7; ++c) ob[c] = ext[c];
+    ob[7] = s[12]; ob[8] = s[13]; ob[9] = s[14];
+    ob[10] = s[9]; ob[11] = s[10]; ob[12] = s[11];
+    ob[13] = s[15]; ob[14] = s[16]; ob[15] = -s[17]; ob[16] = -T.hc.zh(s[17]);
     if (a.list) {
         for (int c = 0; c < 18; ++c)
             if (has_slot(c)) a.state[tix(env, c)] = (float)s[c];
@@ -226,18 +171,42 @@ __device__ __forceinline__ void retrim_write(const RetrimArgs& a, int64_t job, i
     if (a.out_status) a.out_status[job] = HG_OK;
 }
 
-// Lane roles per evaluation round: lanes 0..31 the Jacobian columns at the point the next Newton
-// step will start from, lanes 32..41 the ten step-halving trials of the current step (trial 0,
-// the full step, is that point whenever the search accepts it, which it usually does), lane 32
-// alone the residual at x0 in the first round.  A round is one trim_fcn latency; a trim of three
-// Newton steps takes four rounds.
-__global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
-    __shared__ double gjE[32 * 16];   // the +-eps evaluations of the current Newton step
-    __shared__ double gjR[16];        // its right-hand side y - y*
-    __shared__ double gjS[16];        // its solution
+// One wave per trim.  Each evaluation round evaluates 42 points at once: lanes 0..31 the +-eps
+// Jacobian columns around the point the next Newton step starts from, lanes 32..41 the ten
+// step-halving trials of the current step (trial 0, the full step, is that point whenever the
+// search accepts it, which it usually does; the first round: lane 32 the residual at x0).  The first
+// trial that lowers the residual is the one the reference's sequential search accepts
+// (helicopter_dynamics.py:530-541).  When the search accepts a shorter step, a round of Jacobian
+// lanes alone re-evaluates around it (the trial lanes keep their values).  Then the evaluations go
+// through LDS to the Gauss-Jordan solve.  A trim of three Newton steps takes four rounds and three
+// solves.
+enum : int { kRoundFirst = 0, kRoundNormal = 1, kRoundJacobian = 2 };
+
+// Model constants and trim setup through the constant address space: scalar loads (the kernel's
+// stores cannot alias them), re-issued each round (opaque pointers) instead of hoisted out of the
+// Newton loop, where ~180 fp64 values would stay live in registers.
+typedef __attribute__((address_space(4))) const hg::Params<double> ConstP;
+typedef __attribute__((address_space(4))) const hg::TrimSetup ConstT;
+template <typename Q, typename T>
+__device__ __forceinline__ const T& opaque_const(const T* p) {
+    Q* c = (Q*)p;
+    asm volatile("" : "+s"(c));
+    return *(const T*)c;
+}
+
+#ifndef HG_RETRIM_WAVES
+#define HG_RETRIM_WAVES 2
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WAVES))) void retrim_kernel(const RetrimArgs a) {
+    __shared__ double sE[32 * 16];   // the +-eps evaluations E[j][k] of the current Newton step
+    __shared__ double sR[16];        // its right-hand side y - y*
+    __shared__ double sX[16];        // the solution (Newton direction), by column
+    __shared__ double sExt[7];       // observation terms of the current iterate
     const int l = threadIdx.x;
     const hg::Params<double>& P = *a.P;
     const double eps = hg::kTrimEps;
+    const int c = l & 15;            // Jacobian column of lanes 0..31
+    const int j = l - 32;            // line-search trial of lanes 32..41
     int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
     if (a.count && jobs > a.n) jobs = a.n;   // a queue holds at most one job per env
     for (int64_t job = blockIdx.x; job < jobs; job += gridDim.x) {   // uniform per wave
@@ -250,100 +219,119 @@ __global__ __launch_bounds__(64) void retrim_kernel(const RetrimArgs a) {
             W[1] = (double)wr[1];
             W[2] = (double)wr[2];
         }
-        double x[16], dir[16];
-        for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; }
+        double x[16], dir[16], ye[16], te = 0.0;
+        EvalExt ext;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; ye[k] = 0.0; }
         double tol = 0;
-        int it = 0;
-        bool ok = true, done = false, first = true, have_jac = false;
-        int round = 0;
+        int it = 0, kind = kRoundFirst, src = 32, round = 0;
+        bool ok = true, converged = false;
         RSTAMP(0, "v"(l));
-        while (!done) {
-            // ---- one evaluation round
-            const int c = l & 15;
-            const int j = l - 32;   // line-search trial of this lane (0..9), first round: base point
+        while (true) {
+            const hg::Params<double>& P = opaque_const<ConstP>(a.P);
+            const hg::TrimSetup& T = opaque_const<ConstT>(a.T + (a.setup_stride ? job : 0));
+            // ---- one evaluation round (every x - s dir is the same fused operation wherever formed)
             double xe[16];
-            if (l < 32) {   // Jacobian columns at x - dir (= x in the first round)
-                for (int k = 0; k < 16; ++k) {
-                    const double xs = first ? x[k] : x[k] - 1.0 * dir[k];
-                    xe[k] = k == c ? (l < 16 ? xs + eps : xs - eps) : xs;
-                }
-            } else {
-                const double step = (j >= 0 && j < hg::kTrimLineSearch) ? ldexp(1.0, -j) : 0.0;
-                for (int k = 0; k < 16; ++k) xe[k] = first ? x[k] : x[k] - step * dir[k];
-            }
-            double ye[16], se[18], de[18], oe[17];
-            RSTAMP(1 + 4 * round, "v"(xe[0]));
-            hg::trim_fcn(P, T, xe, W, ye, se, de, oe);
-            const double te = hg::trim_residual(ye, T.yt);
-            RSTAMP(2 + 4 * round, "v"(te));
-            // ---- accept a trial (or take the base point)
-            int src = 32;   // lane whose evaluation is the new iterate
-            if (first) {
-                first = false;
-                have_jac = true;
-            } else {
-                // the first trial (lanes 32 + j) whose residual is below tol: one ballot instead of a
-                // readlane per trial (the reference's sequential search, helicopter_dynamics.py:532-541)
-                const unsigned long long lower = __ballot(j >= 0 && j < hg::kTrimLineSearch && te < tol) >> 32;
-                const int js = lower ? __builtin_ctzll(lower) : hg::kTrimLineSearch;
-                if (js >= hg::kTrimLineSearch - 1) {   // helicopter_dynamics.py:540: keep x
-                    done = true;
-                    src = -1;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const double base = kind == kRoundNormal ? fma(-1.0, dir[k], x[k]) : x[k];
+                double v;
+                if (l < 32) {
+                    v = k == c ? (l < 16 ? base + eps : base - eps) : base;
                 } else {
+                    const double step = (kind == kRoundNormal && j < hg::kTrimLineSearch) ? ldexp(1.0, -j) : 0.0;
+                    v = fma(-step, dir[k], x[k]);
+                }
+                xe[k] = v;
+            }
+            RSTAMP(1 + 4 * round, "v"(xe[0]));
+            if (kind != kRoundJacobian || l < 32) {
+                trim_eval(P, T, xe, W, ye, ext);
+                double t = 0.0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) t = fma(ye[k] - T.yt[k], ye[k] - T.yt[k], t);
+                te = t;
+            }
+            RSTAMP(2 + 4 * round, "v"(te));
+            if (kind != kRoundJacobian) {
+                // ---- accept a trial (or take the base point)
+                bool have_jac = true;
+                if (kind == kRoundNormal) {
+                    const unsigned long long lower = __ballot(j >= 0 && j < hg::kTrimLineSearch && te < tol) >> 32;
+                    const int js = lower ? __builtin_ctzll(lower) : hg::kTrimLineSearch;
+                    if (js >= hg::kTrimLineSearch - 1) break;   // helicopter_dynamics.py:540: keep x
                     const double step = ldexp(1.0, -js);
-                    for (int k = 0; k < 16; ++k) x[k] = x[k] - step * dir[k];
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) x[k] = fma(-step, dir[k], x[k]);
                     src = 32 + js;
                     have_jac = js == 0;   // the Jacobian lanes evaluated around trial 0
-                    if (++it > hg::kTrimMaxIter) { ok = false; done = true; src = -1; }
+                    if (++it > hg::kTrimMaxIter) { ok = false; break; }
                 }
-            }
-            if (src >= 0) {
                 tol = read_lane(te, src);
-                if (!(tol > eps)) {   // converged: the accepting lane holds the final evaluation
-                    done = true;
-                    if (l == src) retrim_write(a, job, env, x, se, oe);
-                    break;
+                if (!(tol > eps)) { converged = true; break; }   // the accepting lane holds the final evaluation
+                if (l == src) {
+#pragma unroll
+                    for (int k = 0; k < 7; ++k) sExt[k] = ext.o[k];
                 }
-            }
-            if (done) break;
-            if (!have_jac) {   // the search accepted a shorter step: Jacobian at the new x
-                if (l < 32) {
-                    for (int k = 0; k < 16; ++k) xe[k] = k == c ? (l < 16 ? x[k] + eps : x[k] - eps) : x[k];
-                    hg::trim_fcn(P, T, xe, W, ye, nullptr, nullptr, nullptr);
+                if (!have_jac) {   // the search accepted a shorter step: Jacobian at the new x first
+                    kind = kRoundJacobian;
+                    ++round;
+                    continue;
                 }
             }
             // ---- Newton direction: the evaluations and the residual (lane src holds y) into LDS,
-            // then Gauss-Jordan over the wave
+            // then the solve, one row per lane
             lds_order();   // the previous solve's reads are done
             if (l < 32) {
 #pragma unroll
-                for (int k = 0; k < 16; ++k) gjE[l * 16 + k] = ye[k];
+                for (int k = 0; k < 16; ++k) sE[l * 16 + k] = ye[k];
             }
             if (l == src) {
 #pragma unroll
-                for (int k = 0; k < 16; ++k) gjR[k] = ye[k] - T.yt[k];
+                for (int k = 0; k < 16; ++k) sR[k] = ye[k] - T.yt[k];
             }
             lds_order();
             RSTAMP(3 + 4 * round, "v"(ye[0]));
-            ok = gauss_jordan_wave(gjE, gjR, gjS, l, job == 0 && round == 0, dir);
-            if (!ok) break;
+            {
+                const int i = l & 15;
+                double A[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) A[q] = (sE[q * 16 + i] - sE[(q + 16) * 16 + i]) * (0.5 / eps);
+                double b = sR[i];
+                bool used = false, bad = false;
+                int mycol = 0;
+                gj_steps<0>(A, b, used, mycol, bad, i);
+                if (l < 16) sX[mycol] = b;
+                lds_order();
+                bool fin = true;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    dir[k] = sX[k];
+                    fin = fin && isfinite(dir[k]);
+                }
+                if (bad || !fin) { ok = false; break; }
+            }
             RSTAMP(4 + 4 * round, "v"(dir[0]));
+            kind = kRoundNormal;
             ++round;
         }
         RSTAMP(63, "v"(l));
-        if (ok && done && l == 0) {
-            // the search stopped without converging (:540): final evaluation at the kept x
-            bool written = !(tol > eps);
-            if (!written) {
-                double yy[16], s[18], d[18], ob[17];
-                hg::trim_fcn(P, T, x, W, yy, s, d, ob);
-                retrim_write(a, job, env, x, s, ob);
+        if (ok) {
+            if (converged) {
+                if (l == src) retrim_write(a, P, T, job, env, x, ext.o);
+            } else if (l == 0) {
+                // the search stopped without converging (:540): the kept x and its evaluation
+                double e[7];
+                lds_order();
+#pragma unroll
+                for (int k = 0; k < 7; ++k) e[k] = sExt[k];
+                retrim_write(a, P, T, job, env, x, e);
             }
-        }
-        if (!ok && l == 0) {
+        } else if (l == 0) {
             if (a.fail_count) atomicAdd(a.fail_count, 1);
             if (a.out_status) a.out_status[job] = HG_E_TRIM;
         }
+        lds_order();   // the next job's writes come after this job's reads
     }
 }
 

@@ -63,15 +63,15 @@ HD void trim_fcn(const Params<double>& P, const TrimSetup& T, const double x[16]
     att.s[2] = T.s_psi;
     att.c[2] = T.c_psi;
     dynamics<true>(P, s, u, W, T.hc, att, d, ob, T.rho_irho);
-    y[0] = d[0] / P.mr_VTIP;
-    y[1] = d[1] / P.tr_VTIP;
+    y[0] = m_div_c(d[0], P.mr_VTIP, P.mr_inv_VTIP);
+    y[1] = m_div_c(d[1], P.tr_VTIP, P.tr_inv_VTIP);
     y[2] = d[4];
     y[3] = d[5];
     for (int i = 0; i < 3; ++i) {
-        y[4 + i] = d[6 + i] / P.mr_VTIP;
-        y[7 + i] = d[9 + i] / P.mr_OMEGA;
+        y[4 + i] = m_div_c(d[6 + i], P.mr_VTIP, P.mr_inv_VTIP);
+        y[7 + i] = m_div_c(d[9 + i], P.mr_OMEGA, P.mr_inv_OMEGA);
         y[10 + i] = d[12 + i];
-        y[13 + i] = d[15 + i] / P.mr_R;
+        y[13 + i] = m_div_c(d[15 + i], P.mr_R, P.mr_inv_R);
     }
     if (s_out)
         for (int i = 0; i < 18; ++i) s_out[i] = s[i];
