@@ -64,6 +64,9 @@ def parse():
                     help="also time hg_rollout (this many steps per launch, same action bank); 0 = off")
     ap.add_argument("--reset-mode", default="template", choices=["template", "retrim"],
                     help="auto-reset state: mean-wind trim template (default) or per-reset device re-trim (F8)")
+    ap.add_argument("--autoreset-mode", default="same_step", choices=["same_step", "next_step"],
+                    help="auto-reset in the step that ends the episode (default) or in the next one (gymnasium)")
+    ap.add_argument("--max-episode-steps", type=int, default=None, help="TimeLimit (gymnasium registry: 5000)")
     ap.add_argument("--graph-steps", type=int, default=100, help="steps captured per hipGraph")
     ap.add_argument("--gather-obs", action="store_true",
                     help="headline = BASELINE config 5: obs gathered to rank 0 every step (needs N > 1)")
@@ -356,7 +359,8 @@ def make_env(args, torch, n, offset, dev):
         return _DryEnv(torch, n, dev)
     from heligym_amd import HeliVecEnv
     env = HeliVecEnv(n, task=args.task, dt=args.dt, seed=1234, autoreset=True, env_offset=offset,
-                     device=dev, reset_mode=args.reset_mode)
+                     device=dev, reset_mode=args.reset_mode, autoreset_mode=args.autoreset_mode,
+                     max_episode_steps=args.max_episode_steps)
     if args.generic_kernel:
         env.set_specialized(False)
     env.reset()
@@ -627,7 +631,7 @@ def main():
         if not args.no_secondary and not args.dry_run:
             # the same step with the compacted reset info (same-step auto-reset: reset indices and
             # terminal observations compacted in-kernel; captured, so a memset node zeroes the count)
-            if args.reset_mode == "template":
+            if args.reset_mode == "template" and args.autoreset_mode == "same_step":
                 def one_step_ri(k):
                     env.step_async(bank[k % B], with_reset_info=True)
                 rep_ri, _k2 = graphs_for(torch, dev, one_step_ri, K, B)
@@ -780,10 +784,13 @@ def main():
         "data": "synthetic: U(-1,1) Philox actions (HBM-resident bank of %d steps), Philox turbulence" % B,
         "config": {"workload": f"{task_name} x {total_envs // world} envs/GPU, Dryden turbulence level 1, "
                                f"dt={args.dt}, auto-reset"
-                               f"{' (re-trim per reset, F8)' if args.reset_mode == 'retrim' else ''}, {mode}"
+                               f"{' (re-trim per reset, F8)' if args.reset_mode == 'retrim' else ''}"
+                               f"{' in the next step' if args.autoreset_mode == 'next_step' else ''}"
+                               f"{f', TimeLimit {args.max_episode_steps}' if args.max_episode_steps else ''}, {mode}"
                                + (", BASELINE config 5" if args.gather_obs else ""),
                    "envs_per_gpu": total_envs // world, "dt": args.dt, "task": args.task,
-                   "reset_mode": args.reset_mode,
+                   "reset_mode": args.reset_mode, "autoreset_mode": args.autoreset_mode,
+                   "max_episode_steps": args.max_episode_steps,
                    "kernel": "specialised (default airframe constants compiled in)" if env.specialized else "generic",
                    "parallelism": f"env-shard x{world}", "world_size_seen": seen_world,
                    "backend": backend or "none (1 rank)"},

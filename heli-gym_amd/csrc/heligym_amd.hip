@@ -114,7 +114,7 @@ struct StepArgs {
     int32_t* reset_index;
     float* final_obs;
     float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
-    int32_t* retrim_list;    // ... compacted ids of the envs to re-trim
+    int4* retrim_recs;       // ... compacted jobs {env, trim wind} of the envs to re-trim
     int32_t* retrim_count;   // ... their number: retrim_count[max(retrim_slot, 0)]
     const float* tmpl_env;   // per-env reset templates [N][39] (Params::env_templates), else unused
 };
@@ -515,7 +515,17 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
             if (lane == leader) base = atomicAdd(a.retrim_count + (a.retrim_slot > 0 ? a.retrim_slot : 0), __popcll(mask));
             base = __shfl(base, leader);
             const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
-            if (do_reset && slot < n) a.retrim_list[slot] = (int32_t)i;
+            if (do_reset && slot < n) {
+                // the job carries its trim wind: this step's (same-step reset), or the one recorded at
+                // the episode's last step (next-step reset)
+                float w0 = W[0], w1 = W[1], w2 = W[2];
+                if (P.autoreset_next) {
+                    w0 = a.retrim_wind[3 * i + 0];
+                    w1 = a.retrim_wind[3 * i + 1];
+                    w2 = a.retrim_wind[3 * i + 2];
+                }
+                a.retrim_recs[slot] = make_int4((int32_t)i, __float_as_int(w0), __float_as_int(w1), __float_as_int(w2));
+            }
         }
     }
     if (FEAT && P.env_templates) {   // this env's own reset target (its own trim condition)
@@ -1056,7 +1066,8 @@ struct hg_env {
     hg::TrimSetup* setup_dev = nullptr;     // ... and device copy (re-trim kernel)
     Params<double>* pd_dev = nullptr;       // fp64 model constants for the re-trim kernel
     float* retrim_wind = nullptr;           // reset_mode RETRIM work buffers
-    int32_t* retrim_list = nullptr;
+    int32_t* retrim_list = nullptr;         // hg_reset's masked envs (their winds by env)
+    int4* retrim_recs = nullptr;            // a step's auto-reset jobs {env, wind}
     int32_t* retrim_count = nullptr;        // [0] jobs of hg_reset's re-trim, [1] failures so far
     int32_t* retrim_ring = nullptr;         // [3] jobs of a step's re-trim: step k counts into [k % 3] and
     uint64_t retrim_gen = 0;                //     zeroes [(k + 1) % 3] from its kernel (no memset launch)
@@ -1331,7 +1342,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if (rc != HG_OK) { delete e; return rc; }
     auto cleanup = [&](hipError_t err, const char* what) {
         dfree(e->hmap); dfree(e->state); dfree(e->az); dfree(e->tmpl_dev); dfree(e->params_dev);
-        dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_count);
+        dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_recs); dfree(e->retrim_count);
         dfree(e->retrim_ring);
         dfree(e->tmpl_env); dfree(e->setup_batch);
         delete e;
@@ -1371,6 +1382,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
             return cleanup(err, "hipMalloc retrim wind");
         if ((err = hipMalloc(&e->retrim_list, sizeof(int32_t) * num_envs)) != hipSuccess)
             return cleanup(err, "hipMalloc retrim list");
+        if ((err = hipMalloc(&e->retrim_recs, sizeof(int4) * num_envs)) != hipSuccess)
+            return cleanup(err, "hipMalloc retrim jobs");
         hipLaunchKernelGGL(fill_wind_kernel, dim3(grid_for(num_envs)), dim3(kBlock), 0, 0, e->retrim_wind, num_envs,
                            (float)e->Pd.wm[0], (float)e->Pd.wm[1], (float)e->Pd.wm[2]);
         if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "fill_wind_kernel");
@@ -1396,6 +1409,7 @@ void hg_destroy(hg_env* e) {
     dfree(e->pd_dev);
     dfree(e->retrim_wind);
     dfree(e->retrim_list);
+    dfree(e->retrim_recs);
     dfree(e->retrim_count);
     dfree(e->retrim_ring);
     dfree(e->tmpl_env);
@@ -1534,7 +1548,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.reset_index = reset_index;
     a.final_obs = final_obs;
     a.retrim_wind = e->retrim_wind;
-    a.retrim_list = e->retrim_list;
+    a.retrim_recs = e->retrim_recs;
     a.retrim_count = retrim ? e->retrim_ring : e->retrim_count;   // (unused unless auto-resets re-trim)
     a.retrim_slot = rt_slot;
     a.tmpl_env = e->tmpl_env;
@@ -1549,8 +1563,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.P = e->pd_dev;
         r.T = e->setup_dev;
         r.count = rt_count;
-        r.list = e->retrim_list;
-        r.wind = e->retrim_wind;
+        r.recs = e->retrim_recs;
         r.state = e->state;
         r.az = e->az;
         r.obs = obs;

@@ -146,7 +146,18 @@ HD float m_rcp(float x) {
     return 1.0f / x;
 #endif
 }
+#if defined(__HIP_DEVICE_COMPILE__)
+// fp64 on the device (the re-trim kernel): v_rcp_f64 and two fused Newton steps (within an ulp for
+// finite non-zero x; the trim model's reciprocals are of cos(theta), 1 + og^2, the fuselage and tail
+// downwash speeds)
+HD double m_rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+#else
 HD double m_rcp(double x) { return 1.0 / x; }
+#endif
 // True when any lane of the wave has `c` (a uniform skip for rarely taken, costly branches).
 HD bool wave_any(bool c) {
 #if defined(__HIP_DEVICE_COMPILE__)

@@ -59,7 +59,8 @@ struct RetrimArgs {
     int32_t setup_stride;   // 0: one trim condition for all jobs; 1: T[job] (hg_trim_conds_batch)
     const int32_t* count;   // env mode: device job count; batch mode: NULL (count = njobs)
     int64_t njobs;
-    const int32_t* list;    // env mode: env id of each job
+    const int32_t* list;    // env mode: env id of each job (winds by env) ...
+    const int4* recs;       // ... or jobs {env, wind bits} (a step's auto-resets)
     const float* wind;      // [N,3] by env id (env mode) or [count,3] by job (batch mode)
     float* state;           // env mode: tiled state (tix; heli 18 and carry 4 rewritten)
     AzRec* az;              // env mode: azimuth records (the trim's azimuths at step 0)

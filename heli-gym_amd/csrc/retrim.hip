@@ -76,17 +76,18 @@ __device__ __forceinline__ uint32_t row16_max(uint32_t k) {
 // Columns < C are neither read nor updated after step C (the host's solve16 updates them and never
 // reads them again).  Fused arithmetic and a different tie rule make this a different rounding of
 // the same solve (the trims are compared with the host's to fp32 resolution, not bitwise).
+// A zero or non-finite pivot (a singular or non-finite system) makes its reciprocal, and with it the
+// solution, non-finite: the caller checks the solution once instead of every pivot.
 template <int C>
-__device__ __forceinline__ void gj_step(double (&A)[16], double& b, bool& used, int& mycol, bool& bad, int i) {
+__device__ __forceinline__ void gj_step(double (&A)[16], double& b, uint32_t& live, int& mycol, int i) {
     const double v = A[C];
-    const uint32_t hi = (uint32_t)(__double_as_longlong(v) >> 32) & 0x7FFFFFFFu;
-    const uint32_t key = used ? 0u : hi;
+    // |v|'s high word with the top bit set (so that a zero candidate still beats a used row); 0 once used
+    const uint32_t key = ((uint32_t)(__double_as_longlong(v) >> 32) | 0x80000000u) & live;
+    const double own_inv = rcp_f64(v);   // every row's reciprocal while the search runs (off its chain)
     const uint32_t mx = row16_max(key);
     const uint32_t hit = (uint32_t)__ballot(key == mx) & 0xFFFFu;   // rows of the first 16 lanes
     const int P = __builtin_ctz(hit | 0x10000u);
-    const double mp = read_lane(v, P);
-    bad = bad || mx == 0u || !isfinite(mp);
-    const double rinv = rcp_f64(mp);
+    const double rinv = read_lane(own_inv, P);
     const bool piv = i == P;
     // other rows: A - (v / pivot) pj; the pivot row: A / pivot -- one form for both, A * m - g pj with
     // (m, g) = (1, v / pivot) or (1 / pivot, 0): the product by 1 and the fused add of -0 are exact
@@ -95,13 +96,13 @@ __device__ __forceinline__ void gj_step(double (&A)[16], double& b, bool& used, 
 #pragma unroll
     for (int j = C + 1; j < 16; ++j) A[j] = fma(-g, read_lane(A[j], P), A[j] * m);
     b = fma(-g, read_lane(b, P), b * m);
-    used = used || piv;
+    live = piv ? 0u : live;
     mycol = piv ? C : mycol;
 }
 template <int C>
-__device__ __forceinline__ void gj_steps(double (&A)[16], double& b, bool& used, int& mycol, bool& bad, int i) {
-    gj_step<C>(A, b, used, mycol, bad, i);
-    if constexpr (C < 15) gj_steps<C + 1>(A, b, used, mycol, bad, i);
+__device__ __forceinline__ void gj_steps(double (&A)[16], double& b, uint32_t& live, int& mycol, int i) {
+    gj_step<C>(A, b, live, mycol, i);
+    if constexpr (C < 15) gj_steps<C + 1>(A, b, live, mycol, i);
 }
 
 // What the observation needs from one evaluation beyond the state: power, uvw_air, ned velocity
@@ -151,7 +152,7 @@ __device__ __forceinline__ void retrim_write(const RetrimArgs& a, const hg::Para
     ob[7] = s[12]; ob[8] = s[13]; ob[9] = s[14];
     ob[10] = s[9]; ob[11] = s[10]; ob[12] = s[11];
     ob[13] = s[15]; ob[14] = s[16]; ob[15] = -s[17]; ob[16] = -T.hc.zh(s[17]);
-    if (a.list) {
+    if (a.list || a.recs) {
         for (int c = 0; c < 18; ++c)
             if (has_slot(c)) a.state[tix(env, c)] = (float)s[c];
         const int32_t epi = reinterpret_cast<const int32_t*>(a.state)[tix(env, kCtrCol0 + 2)];
@@ -207,13 +208,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WA
     const double eps = hg::kTrimEps;
     const int c = l & 15;            // Jacobian column of lanes 0..31
     const int j = l - 32;            // line-search trial of lanes 32..41
+    // the first job record is requested with the job count (the grid never exceeds the list: blocks
+    // <= min(n, 1024)), so the start waits for one load, not two dependent ones
+    const int4 rec0 = a.recs ? a.recs[blockIdx.x] : make_int4(0, 0, 0, 0);
     int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
     if (a.count && jobs > a.n) jobs = a.n;   // a queue holds at most one job per env
     for (int64_t job = blockIdx.x; job < jobs; job += gridDim.x) {   // uniform per wave
-        const int64_t env = a.list ? (int64_t)a.list[job] : job;
+        const int4 rec = a.recs ? (job == blockIdx.x ? rec0 : a.recs[job]) : make_int4(0, 0, 0, 0);
+        const int64_t env = a.recs ? (int64_t)rec.x : (a.list ? (int64_t)a.list[job] : job);
         const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];
         double W[3] = {P.wm[0], P.wm[1], P.wm[2]};   // NULL wind: the mean wind (helicopter.py:55)
-        if (a.wind) {
+        if (a.recs) {
+            W[0] = (double)__int_as_float(rec.y);
+            W[1] = (double)__int_as_float(rec.z);
+            W[2] = (double)__int_as_float(rec.w);
+        } else if (a.wind) {
             const float* wr = a.wind + 3 * (a.list ? env : job);
             W[0] = (double)wr[0];
             W[1] = (double)wr[1];
@@ -294,13 +303,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WA
             RSTAMP(3 + 4 * round, "v"(ye[0]));
             {
                 const int i = l & 15;
-                double A[16];
+                double A[16], Em[16];
 #pragma unroll
-                for (int q = 0; q < 16; ++q) A[q] = (sE[q * 16 + i] - sE[(q + 16) * 16 + i]) * (0.5 / eps);
+                for (int q = 0; q < 16; ++q) {   // all 33 reads issued before the first use
+                    A[q] = sE[q * 16 + i];
+                    Em[q] = sE[(q + 16) * 16 + i];
+                }
                 double b = sR[i];
-                bool used = false, bad = false;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) A[q] = (A[q] - Em[q]) * (0.5 / eps);
+                uint32_t live = 0xFFFFFFFFu;   // the key mask of a row not yet used as a pivot
                 int mycol = 0;
-                gj_steps<0>(A, b, used, mycol, bad, i);
+                gj_steps<0>(A, b, live, mycol, i);
                 if (l < 16) sX[mycol] = b;
                 lds_order();
                 bool fin = true;
@@ -309,7 +323,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WA
                     dir[k] = sX[k];
                     fin = fin && isfinite(dir[k]);
                 }
-                if (bad || !fin) { ok = false; break; }
+                if (!fin) { ok = false; break; }
             }
             RSTAMP(4 + 4 * round, "v"(dir[0]));
             kind = kRoundNormal;
