@@ -113,7 +113,7 @@ struct StepArgs {
     int32_t* reset_count_next;   // zeroed by this launch for a later step (hg_step_chained), or NULL
     int32_t* reset_index;
     float* final_obs;
-    float* retrim_wind;      // reset_mode RETRIM: [N,3] wind of the step (the trim wind of a reset)
+    float* retrim_wind;      // reset_mode RETRIM: [3][N] wind of the step (the trim wind of a reset)
     int4* retrim_recs;       // ... compacted jobs {env, trim wind} of the envs to re-trim
     int32_t* retrim_count;   // ... their number: retrim_count[max(retrim_slot, 0)]
     const float* tmpl_env;   // per-env reset templates [N][39] (Params::env_templates), else unused
@@ -293,7 +293,7 @@ __device__ __forceinline__ void draw_eta(const StepArgs& a, uint64_t seed, int64
 
 #if HG_TIMING
 #define HG_TIMING_WAVES 2048
-#define HG_TIMING_SLOTS 16
+#define HG_TIMING_SLOTS 17   // 0..13 phase stamps, 14/15 realtime end/start, 16 the wave's branch flags
 __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
 #define TSTAMP(j, ...)                                                                          \
     do {                                                                                        \
@@ -309,6 +309,13 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
         const int w_ = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);                    \
         if ((threadIdx.x & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;              \
+    } while (0)
+// which wave-uniform branches the wave took (HG_TIMING builds): 1 reset, 2 gear contact code,
+// 4 the full sincos of a large attitude increment
+#define HG_STAGE_FLAG(bit)                                                                      \
+    do {                                                                                        \
+        const int w_ = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);                    \
+        if ((threadIdx.x & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][16] |= (bit);         \
     } while (0)
 #else
 #define TSTAMP(j, ...) do { } while (0)
@@ -355,7 +362,10 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
 #define GRP(ptr, g) ((ptr) + ((g) - 4) * kTileEnvs)
 
 #if HG_TIMING
-    if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][15] = __builtin_amdgcn_s_memrealtime();
+    if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) {
+        g_timing[i >> 6][15] = __builtin_amdgcn_s_memrealtime();
+        g_timing[i >> 6][16] = 0;
+    }
 #endif
     TSTAMP(0, "v"(tid));
     // reset template (heli[18] | carry[4] | obs[17]) one float per lane, requested with the state so
@@ -420,10 +430,10 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
 #endif
     TSTAMP(8, "v"(hs[8]), "v"(hs[11]), "v"(obs[16]));
     if (FEAT && P.reset_retrim && active && !(P.autoreset_next && step < 0)) {   // F8: a reset trims against this wind
-        float* wb = a.retrim_wind + 3 * blk0;
-        st_lane<false>(wb + 0, 3 * (uint32_t)tid, W[0]);
-        st_lane<false>(wb + 1, 3 * (uint32_t)tid, W[1]);
-        st_lane<false>(wb + 2, 3 * (uint32_t)tid, W[2]);
+        float* wb = a.retrim_wind + blk0;   // [3][N]: three coalesced rows
+        st_lane<false>(wb, (uint32_t)tid, W[0]);
+        st_lane<false>(wb + n, (uint32_t)tid, W[1]);
+        st_lane<false>(wb + 2 * n, (uint32_t)tid, W[2]);
     }
     // step_after (helicopter_dynamics.py:73-77)
     // utils.py pi_bound, (x + pi) % 2pi - pi.  An angle already in [-pi, pi) is kept as is -- what
@@ -520,9 +530,9 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
                 // the episode's last step (next-step reset)
                 float w0 = W[0], w1 = W[1], w2 = W[2];
                 if (P.autoreset_next) {
-                    w0 = a.retrim_wind[3 * i + 0];
-                    w1 = a.retrim_wind[3 * i + 1];
-                    w2 = a.retrim_wind[3 * i + 2];
+                    w0 = a.retrim_wind[i];
+                    w1 = a.retrim_wind[n + i];
+                    w2 = a.retrim_wind[2 * n + i];
                 }
                 a.retrim_recs[slot] = make_int4((int32_t)i, __float_as_int(w0), __float_as_int(w1), __float_as_int(w2));
             }
@@ -539,6 +549,9 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
             for (int c = 0; c < 17; ++c) obs[c] = tr[22 + c];
         }
     } else if (__ballot(do_reset)) {
+#if HG_TIMING
+        HG_STAGE_FLAG(1);
+#endif
         // Template<float> = heli[18] | carry[4] | obs[17], float c held by lane c.  The readlanes run
         // in this wave-uniform branch (every lane has loaded its template float), the selects per lane.
 #pragma unroll
@@ -603,9 +616,9 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
 __global__ __launch_bounds__(kBlock) void fill_wind_kernel(float* wind, int64_t n, float w0, float w1, float w2) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    wind[3 * i + 0] = w0;
-    wind[3 * i + 1] = w1;
-    wind[3 * i + 2] = w2;
+    wind[i] = w0;   // [3][N]
+    wind[n + i] = w1;
+    wind[2 * n + i] = w2;
 }
 
 __global__ __launch_bounds__(kBlock) void mask_list_kernel(const uint8_t* mask, int64_t n, int32_t* list,
@@ -1158,9 +1171,12 @@ static int32_t build_template(hg_env* e) {
 }
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
-// re-trim launches: one job per 64-lane block, at most 1024 blocks (jobs beyond loop)
+// re-trim launches: one job per 64-lane block, at most HG_RETRIM_GRID blocks (jobs beyond loop)
+#ifndef HG_RETRIM_GRID
+#define HG_RETRIM_GRID 1024
+#endif
 static inline unsigned retrim_grid(int64_t jobs) {
-    return (unsigned)(jobs < 1 ? 1 : (jobs > 1024 ? 1024 : jobs));
+    return (unsigned)(jobs < 1 ? 1 : (jobs > HG_RETRIM_GRID ? HG_RETRIM_GRID : jobs));
 }
 
 #define PARAM_ARG(e) ((const Params<float>*)(e)->params_dev)
@@ -1480,6 +1496,7 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
         r.count = e->retrim_count;
         r.list = e->retrim_list;
         r.wind = e->retrim_wind;
+        r.wind_soa = 1;
         r.state = e->state;
         r.az = e->az;
         r.obs = obs;

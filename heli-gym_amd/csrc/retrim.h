@@ -61,7 +61,8 @@ struct RetrimArgs {
     int64_t njobs;
     const int32_t* list;    // env mode: env id of each job (winds by env) ...
     const int4* recs;       // ... or jobs {env, wind bits} (a step's auto-resets)
-    const float* wind;      // [N,3] by env id (env mode) or [count,3] by job (batch mode)
+    const float* wind;      // [N,3] by env id (env mode) or [count,3] by job (batch mode) ...
+    int32_t wind_soa;       // ... or [3][N] by env id (env mode: the step's per-env wind records)
     float* state;           // env mode: tiled state (tix; heli 18 and carry 4 rewritten)
     AzRec* az;              // env mode: azimuth records (the trim's azimuths at step 0)
     float* obs;             // env mode: [N,17] reset observation rows, or NULL

@@ -78,8 +78,18 @@ __device__ __forceinline__ uint32_t row16_max(uint32_t k) {
 // the same solve (the trims are compared with the host's to fp32 resolution, not bitwise).
 // A zero or non-finite pivot (a singular or non-finite system) makes its reciprocal, and with it the
 // solution, non-finite: the caller checks the solution once instead of every pivot.
+#ifndef HG_GJ_NOSCALE   // 1: the pivot rows stay unscaled, each row's solution divided at the end
+#define HG_GJ_NOSCALE 0
+#endif
+#ifndef HG_GJ_LDS       // 1: the pivot row reaches the other rows through LDS (broadcast reads)
+#define HG_GJ_LDS 0
+#endif
+constexpr int kRowStride = 18;   // doubles per LDS row (16-byte aligned pairs)
+
 template <int C>
-__device__ __forceinline__ void gj_step(double (&A)[16], double& b, uint32_t& live, int& mycol, int i) {
+__device__ __forceinline__ void gj_step(double (&A)[16], double& b, uint32_t& live, int& mycol, int i,
+                                        double& myinv, double* sRow, int l) {
+    (void)myinv; (void)sRow; (void)l;
     const double v = A[C];
     // |v|'s high word with the top bit set (so that a zero candidate still beats a used row); 0 once used
     const uint32_t key = ((uint32_t)(__double_as_longlong(v) >> 32) | 0x80000000u) & live;
@@ -89,20 +99,60 @@ __device__ __forceinline__ void gj_step(double (&A)[16], double& b, uint32_t& li
     const int P = __builtin_ctz(hit | 0x10000u);
     const double rinv = read_lane(own_inv, P);
     const bool piv = i == P;
+#if HG_GJ_LDS
+    // every row's live part to its LDS row, then the pivot row read back by all (broadcast)
+    constexpr int k0 = (C + 1) >> 1;
+    double* mine = sRow + l * kRowStride;
+#pragma unroll
+    for (int k = k0; k < 8; ++k) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<d2*>(mine + 2 * k) = d2{A[2 * k], A[2 * k + 1]};
+    }
+    mine[16] = b;
+    lds_order();
+    double pr[17];
+    const double* prow = sRow + P * kRowStride;
+#pragma unroll
+    for (int k = k0; k < 8; ++k) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const d2 t = *reinterpret_cast<const d2*>(prow + 2 * k);
+        pr[2 * k] = t.x;
+        pr[2 * k + 1] = t.y;
+    }
+    pr[16] = prow[16];
+#define HG_PJ(j) pr[j]
+#define HG_PB pr[16]
+#else
+#define HG_PJ(j) read_lane(A[j], P)
+#define HG_PB read_lane(b, P)
+#endif
+#if HG_GJ_NOSCALE
+    // rows are never scaled: other rows subtract (v / pivot) x the pivot row, the pivot row keeps its
+    // values (the fused add of -0 is exact) and its reciprocal divides its right-hand side at the end
+    const double g = piv ? 0.0 : v * rinv;
+#pragma unroll
+    for (int j = C + 1; j < 16; ++j) A[j] = fma(-g, HG_PJ(j), A[j]);
+    b = fma(-g, HG_PB, b);
+    myinv = piv ? rinv : myinv;
+#else
     // other rows: A - (v / pivot) pj; the pivot row: A / pivot -- one form for both, A * m - g pj with
     // (m, g) = (1, v / pivot) or (1 / pivot, 0): the product by 1 and the fused add of -0 are exact
     const double g = piv ? 0.0 : v * rinv;
     const double m = piv ? rinv : 1.0;
 #pragma unroll
-    for (int j = C + 1; j < 16; ++j) A[j] = fma(-g, read_lane(A[j], P), A[j] * m);
-    b = fma(-g, read_lane(b, P), b * m);
+    for (int j = C + 1; j < 16; ++j) A[j] = fma(-g, HG_PJ(j), A[j] * m);
+    b = fma(-g, HG_PB, b * m);
+#endif
+#undef HG_PJ
+#undef HG_PB
     live = piv ? 0u : live;
     mycol = piv ? C : mycol;
 }
 template <int C>
-__device__ __forceinline__ void gj_steps(double (&A)[16], double& b, uint32_t& live, int& mycol, int i) {
-    gj_step<C>(A, b, live, mycol, i);
-    if constexpr (C < 15) gj_steps<C + 1>(A, b, live, mycol, i);
+__device__ __forceinline__ void gj_steps(double (&A)[16], double& b, uint32_t& live, int& mycol, int i,
+                                         double& myinv, double* sRow, int l) {
+    gj_step<C>(A, b, live, mycol, i, myinv, sRow, l);
+    if constexpr (C < 15) gj_steps<C + 1>(A, b, live, mycol, i, myinv, sRow, l);
 }
 
 // What the observation needs from one evaluation beyond the state: power, uvw_air, ned velocity
@@ -203,6 +253,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WA
     __shared__ double sR[16];        // its right-hand side y - y*
     __shared__ double sX[16];        // the solution (Newton direction), by column
     __shared__ double sExt[7];       // observation terms of the current iterate
+    __shared__ double sRow[HG_GJ_LDS ? 64 * kRowStride : 2];   // HG_GJ_LDS: the rows of the solve
     const int l = threadIdx.x;
     const hg::Params<double>& P = *a.P;
     const double eps = hg::kTrimEps;
@@ -222,6 +273,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WA
             W[0] = (double)__int_as_float(rec.y);
             W[1] = (double)__int_as_float(rec.z);
             W[2] = (double)__int_as_float(rec.w);
+        } else if (a.wind && a.wind_soa) {
+            W[0] = (double)a.wind[env];
+            W[1] = (double)a.wind[a.n + env];
+            W[2] = (double)a.wind[2 * a.n + env];
         } else if (a.wind) {
             const float* wr = a.wind + 3 * (a.list ? env : job);
             W[0] = (double)wr[0];
@@ -314,8 +369,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WA
                 for (int q = 0; q < 16; ++q) A[q] = (A[q] - Em[q]) * (0.5 / eps);
                 uint32_t live = 0xFFFFFFFFu;   // the key mask of a row not yet used as a pivot
                 int mycol = 0;
-                gj_steps<0>(A, b, live, mycol, i);
-                if (l < 16) sX[mycol] = b;
+                double myinv = 1.0;
+                gj_steps<0>(A, b, live, mycol, i, myinv, sRow, l);
+                if (l < 16) sX[mycol] = HG_GJ_NOSCALE ? b * myinv : b;
                 lds_order();
                 bool fin = true;
 #pragma unroll

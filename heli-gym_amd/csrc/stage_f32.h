@@ -28,6 +28,9 @@
 
 #include "physics.h"
 
+#ifndef HG_STAGE_FLAG    // diagnostic branch flags (HG_TIMING builds of heligym_amd.hip)
+#define HG_STAGE_FLAG(bit) do { } while (0)
+#endif
 #ifndef HG_STAGE_STAMP   // diagnostic phase stamps (HG_TIMING builds of heligym_amd.hip)
 #define HG_STAGE_STAMP(j, ...) do { } while (0)
 #endif
@@ -287,6 +290,7 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
 #else
     if (false) {
 #endif
+        HG_STAGE_FLAG(4);
         if (!small) {
             a.a[0] = sincos2(pp.x);
             a.a[1] = sincos2(th);
@@ -424,6 +428,7 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
 #else
     if (false) {
 #endif
+        HG_STAGE_FLAG(2);
         const float zh = c.g.zh(z);
         const f2 B22 = B12;
         float Fl0 = 0.f, Fl1 = 0.f, Fl2 = 0.f, Ml0 = 0.f, Ml1 = 0.f, Ml2 = 0.f;

@@ -20,7 +20,7 @@ ORDER = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 11, 12]   # stamp slots in progra
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
-    ap.add_argument("--warm", type=int, default=300)
+    ap.add_argument("--warm", type=int, default=3000, help="steps before the recorded launch (aged population)")
     ap.add_argument("--dt", type=float, default=0.01)
     args = ap.parse_args()
     import torch
@@ -32,7 +32,7 @@ def main():
         env.random_actions(act, seed=1, step=k)
         env.step_async(act, with_reset_info=False)
     torch.cuda.synchronize()
-    buf = np.zeros((2048, 16), dtype=np.uint64)
+    buf = np.zeros((2048, 17), dtype=np.uint64)
     fn = env.lib.hg_debug_timing
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     assert fn(buf.ctypes.data, buf.nbytes) == 0
@@ -52,6 +52,17 @@ def main():
     for j, name in enumerate(PHASES):
         print(f"  {name:24s} median {np.median(d[:, j]):6.3f} us   p90 {np.percentile(d[:, j], 90):6.3f} us   "
               f"max {d[:, j].max():6.3f} us")
+    # which wave-uniform branches the waves took, and how long those waves lived
+    fl = buf[:nw, 16].astype(np.int64)
+    names = {1: "reset", 2: "gear contact", 4: "full sincos"}
+    print(f"branch flags: " + ", ".join(f"{v} {int(((fl & b) != 0).sum())} waves" for b, v in names.items()))
+    for cls, sel in (("no branch", fl == 0), ("reset only", fl == 1), ("gear", (fl & 2) != 0),
+                     ("full sincos", (fl & 4) != 0)):
+        if sel.any():
+            print(f"  {cls:12s} {int(sel.sum()):5d} waves: life median {np.median(span_ns[sel])/1e3:.2f} us, "
+                  f"max {span_ns[sel].max()/1e3:.2f} us; end median {np.median(ends[sel])/1e3:.2f} max {ends[sel].max()/1e3:.2f} us")
+    last = np.argsort(ends)[-20:]
+    print("the 20 last-ending waves: flags", fl[last].tolist(), "start", np.round(starts[last] / 1e3, 2).tolist())
     env.close()
 
 
