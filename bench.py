@@ -498,6 +498,42 @@ def gather_graphs(torch, dist, env, bank, B, K, rank, world, dev):
     return replay, (full, rest, bufs, gls, cap, side), G
 
 
+def airframes(args, torch, timer, N, dev, B, K, R, head_s):
+    """Row f4's other airframes at headline speed: the heavier airframe with other rotor speeds and
+    the winged one (tests/golden traj_var_* documents), stepped with the generic kernel and then with
+    the kernel specialised for their constants at run time (HeliVecEnv.specialize, heligym_amd._rtc),
+    against the default airframe's compiled-in kernel (the headline)."""
+    import golden_cases as gc
+    from heligym_amd import HeliVecEnv
+    out = {}
+    for name in ("heavy", "wing"):
+        doc = gc.load_variant(name)[1]
+        env = HeliVecEnv(N, task=args.task, dt=args.dt, seed=1234, autoreset=True, heli_name=doc, device=dev)
+        env.reset()
+        bank = action_bank(args, torch, env, N, dev, B)
+        age(args, torch, env, bank, B)
+
+        def one(k):
+            env.step_async(bank[k % B], with_reset_info=False)
+        rep, keep = graphs_for(torch, dev, one, K, B)
+        s_g, _, _, rs_g = timer.run_counted(env, rep, R)
+        del keep
+        t0 = time.perf_counter()
+        spec = env.specialize()
+        t_build = time.perf_counter() - t0
+        rep, keep = graphs_for(torch, dev, one, K, B)
+        s_s, _, _, rs_s = timer.run_counted(env, rep, R)
+        del keep
+        out[name] = {"generic_ms_per_step": s_g / K * 1e3, "specialised_ms_per_step": s_s / K * 1e3,
+                     "specialised": spec, "specialise_s": t_build,
+                     "specialised_over_default_airframe": (s_s / K) / head_s,
+                     "resets_in_window": [rs_g, rs_s]}
+        env.close()
+    out["note"] = ("specialise_s: hipcc --genco of csrc/step_rtc.hip with the airframe's constants (0 when "
+                   "cached); specialised_over_default_airframe: against the headline's compiled-in AW109 kernel")
+    return out
+
+
 def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev, backend):
     """BASELINE config 5 on this rank's shard: the gather loop (hipGraphs of steps + RCCL gathers, or
     eager where capture is unavailable) and the plain (graph) steps."""
@@ -683,6 +719,11 @@ def main():
                 secondary["generic_kernel"] = {"kernel": "generic (constants loaded, any airframe)",
                                                "value": total_envs * K / s_g, "unit": "env-steps/s",
                                                "ms_per_step": s_g / K * 1e3, "resets_in_window": rs_g}
+            if world == 1 and args.task != "heli" and args.reset_mode == "template" and N <= 262144:
+                try:
+                    secondary["airframes"] = airframes(args, torch, timer, N, dev, B, K, R, sec / K)
+                except Exception as exc:   # (hipcc missing, ...): report, never lose the line
+                    secondary["airframes"] = {"error": repr(exc)}
             if args.rollout_steps > 0 and args.reset_mode == "template":
                 Rs = args.rollout_steps
                 rbank = bank if Rs == B else torch.stack([bank[k % B] for k in range(Rs)])

@@ -54,8 +54,12 @@ struct ParamWords {
 static_assert(sizeof(ParamWords) == sizeof(Params<float>), "Params<float> must be whole dwords");
 
 // derive<float>() of the default config (baked fields only; the rest are zero)
+// HG_BAKED_INC: another airframe's image, for the run-time specialised code objects (step_rtc.hip)
+#ifndef HG_BAKED_INC
+#define HG_BAKED_INC "baked_aw109.inc"
+#endif
 constexpr Params<float> kBakedAW109 = __builtin_bit_cast(Params<float>, ParamWords{{
-#include "baked_aw109.inc"
+#include HG_BAKED_INC
 }});
 
 #define HG_FIELD_BYTES(f) +sizeof(((const Params<float>*)nullptr)->f)
@@ -74,10 +78,11 @@ HD Params<float> bake(const Params<float>& R) {
     return P;
 }
 
-// True when every baked field of P equals the compiled-in value bit for bit.
-inline bool bake_matches(const Params<float>& P) {
+// True when every baked field of P equals that of the constant image I (default: the compiled-in
+// one) bit for bit.
+inline bool bake_matches(const Params<float>& P, const Params<float>& I = kBakedAW109) {
     bool ok = true;
-#define HG_BAKE_CMP(f) ok = ok && memcmp(&P.f, &kBakedAW109.f, sizeof(P.f)) == 0;
+#define HG_BAKE_CMP(f) ok = ok && memcmp(&P.f, &I.f, sizeof(P.f)) == 0;
     HG_BAKED_FIELDS(HG_BAKE_CMP)
 #undef HG_BAKE_CMP
     return ok;

@@ -332,10 +332,11 @@ namespace {
 // kept in registers between them; BAKED: the default airframe's model constants compiled in as
 // instruction literals (baked.h), the runtime fields still read from the device copy.  All
 // compile-time, so the hot kernel has no data-independent branches to merge around.
+// The body is a device function so that the run-time specialised code objects (step_rtc.hip) wrap
+// the same code in kernels of their own names.
 template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool NTS>
-__global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p,
-                                                      int64_t envoff_p, ParamArg Pa,
-                                                      const Template<float>* __restrict__ Tp, const StepArgs a) {
+__device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p,
+                                          ParamArg Pa, const Template<float>* __restrict__ Tp, const StepArgs& a) {
     __shared__ float s_obs[kStepBlock * HG_N_OBS];   // one 64-row slice per wave
     constexpr bool kNTS = NT || NTS;   // non-temporal output stores
     const Params<float>& P0 = *Pa;   // model constants: scalar loads from a device copy
@@ -610,6 +611,17 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
     if ((tid & 63) == 0 && (i >> 6) < HG_TIMING_WAVES) g_timing[i >> 6][14] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
+
+template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool NTS>
+__global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p,
+                                                      int64_t envoff_p, ParamArg Pa,
+                                                      const Template<float>* __restrict__ Tp, const StepArgs a) {
+    step_body<TASK, ETA, NT, FEAT, MULTI, BAKED, NTS>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a);
+}
+
+#ifdef HG_RTC   // step_rtc.hip: the step kernel's code and nothing else
+}  // namespace
+#else
 
 // reset_mode RETRIM bookkeeping: the wind each env's next reset is trimmed against (the mean wind
 // until the env has stepped, helicopter.py:55), and the compacted list of masked envs of hg_reset.
@@ -1089,6 +1101,12 @@ struct hg_env {
     bool env_templates = false;
     bool baked = false;                     // step with the constant-specialised kernel (baked.h)
     bool baked_allowed = true;              // ... unless switched off (hg_set_specialized)
+    // a run-time specialised code object for another airframe (step_rtc.hip, hg_load_specialized)
+    hipModule_t rtc_mod = nullptr;
+    hipFunction_t rtc_fn[6] = {};           // nt, nt_feat, nts, nts_feat, bulk, bulk_feat
+    Params<float> rtc_image;                // the constant image it was built with
+    int32_t rtc_task = -1;
+    bool rtc = false;                       // in use: its image matches this env's constants
     hg::TrimSetup* setup_batch = nullptr;   // hg_trim_conds_batch scratch
     uint64_t chain_expect = kChainBroken;   // chain key of the previous step launch if it was a chained one
     bool ever_captured = false;             // a step was captured into a graph: replays the host cannot see may
@@ -1118,6 +1136,8 @@ static void rederive(hg_env* e) {
     e->Pf = derive<float>(e->cfg, e->rows, e->cols);
     e->Pf.env_templates = e->env_templates ? 1 : 0;
     e->baked = e->baked_allowed && hg::bake_matches(e->Pf);
+    e->rtc = !e->baked && e->baked_allowed && e->rtc_mod && e->rtc_task == e->cfg.task &&
+             hg::bake_matches(e->Pf, e->rtc_image);
 }
 
 // Upload the fp32 model constants the step kernel reads (after create and every setter).
@@ -1204,6 +1224,19 @@ static void launch_step(const hg_env* e, hipStream_t s, const StepArgs& a) {
 // it; with or without the optional features.
 template <int T, bool MULTI>
 static void dispatch_step(const hg_env* e, hipStream_t s, const StepArgs& a, bool eta, bool feat) {
+    if (!MULTI && !eta && e->rtc) {   // the airframe's run-time specialised kernels, same size rules
+        const int v = e->n <= HG_NT_WAVES * e->resident_envs ? 0 : (e->n <= HG_NTS_WAVES * e->resident_envs ? 2 : 4);
+        float* state = e->state;
+        int64_t n = e->n, off = (int64_t)e->cfg.env_offset;
+        uint64_t seed = (uint64_t)e->cfg.seed;
+        const Params<float>* pa = PARAM_ARG(e);
+        const Template<float>* tp = e->tmpl_dev;
+        StepArgs args = a;
+        void* params[] = {&state, &n, &seed, &off, &pa, &tp, &args};
+        const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock);
+        (void)hipModuleLaunchKernel(e->rtc_fn[v + (feat ? 1 : 0)], grid, 1, 1, kStepBlock, 1, 1, 0, s, params, nullptr);
+        return;
+    }
     auto pick = [&](auto nt) {
         constexpr bool NT = decltype(nt)::value;
         if (e->baked) {
@@ -1416,6 +1449,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
 void hg_destroy(hg_env* e) {
     if (!e) return;
     DevGuard dev_guard(e);
+    if (e->rtc_mod) (void)hipModuleUnload(e->rtc_mod);
     dfree(e->hmap);
     dfree(e->state);
     dfree(e->az);
@@ -1448,7 +1482,34 @@ int32_t hg_set_specialized(hg_env* e, int32_t enable) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     e->baked_allowed = enable != 0;
     rederive(e);
-    return e->baked ? 1 : 0;
+    return (e->baked || e->rtc) ? 1 : 0;
+}
+
+int32_t hg_load_specialized(hg_env* e, const char* code_object, int32_t task, const void* image, int64_t bytes) {
+    if (!e || !code_object || !image) return fail(HG_E_INVALID, "hg_load_specialized: NULL argument");
+    if (bytes != (int64_t)sizeof(Params<float>)) return fail(HG_E_INVALID, "hg_load_specialized: image size mismatch");
+    DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
+    hipModule_t mod = nullptr;
+    HIP_TRY(hipModuleLoad(&mod, code_object));
+    static const char* const names[6] = {"hg_rtc_step_nt", "hg_rtc_step_nt_feat", "hg_rtc_step_nts",
+                                         "hg_rtc_step_nts_feat", "hg_rtc_step_bulk", "hg_rtc_step_bulk_feat"};
+    hipFunction_t fn[6];
+    for (int k = 0; k < 6; ++k) {
+        const hipError_t err = hipModuleGetFunction(&fn[k], mod, names[k]);
+        if (err != hipSuccess) {
+            (void)hipModuleUnload(mod);
+            return fail(HG_E_HIP, std::string("hg_load_specialized: ") + names[k] + ": " + hipGetErrorString(err));
+        }
+    }
+    HIP_TRY(hipDeviceSynchronize());   // queued steps may still use a previous module
+    if (e->rtc_mod) (void)hipModuleUnload(e->rtc_mod);
+    e->rtc_mod = mod;
+    for (int k = 0; k < 6; ++k) e->rtc_fn[k] = fn[k];
+    memcpy(&e->rtc_image, image, sizeof(e->rtc_image));
+    e->rtc_task = task;
+    rederive(e);
+    return e->rtc ? 1 : 0;
 }
 
 int32_t hg_set_target(hg_env* e, const hg_target* t) {
@@ -1773,3 +1834,5 @@ int32_t hg_random_actions(hg_env* e, float* actions, uint64_t seed, uint64_t ste
 }
 
 }  // extern "C"
+
+#endif  // HG_RTC

@@ -91,6 +91,7 @@ _SIGS = {
     "hg_set_max_time": (ctypes.c_int32, [_P, ctypes.c_double]),
     "hg_set_target": (ctypes.c_int32, [_P, ctypes.POINTER(hg_target)]),
     "hg_set_specialized": (ctypes.c_int32, [_P, ctypes.c_int32]),
+    "hg_load_specialized": (ctypes.c_int32, [_P, ctypes.c_char_p, ctypes.c_int32, _P, ctypes.c_int64]),
     "hg_set_trim_cond": (ctypes.c_int32, [_P, ctypes.POINTER(hg_trim_cond)]),
     "hg_get_template": (ctypes.c_int32, [_P, ctypes.POINTER(hg_trim_result)]),
     "hg_reset": (ctypes.c_int32, [_P, _P, _P, _P]),

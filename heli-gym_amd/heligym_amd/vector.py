@@ -164,7 +164,7 @@ class HeliVecEnv(*_VEC_BASES):
     def __init__(self, num_envs, task="hover", dt=config.DT, heli_name="aw109", seed=0, device=None,
                  autoreset=True, env_offset=0, max_time=None, target=None, trim_cond=None,
                  turbulence_level=None, reset_mode="template", autoreset_mode="same_step",
-                 max_episode_steps=None, terrain=None):
+                 max_episode_steps=None, terrain=None, specialize=False):
         import torch
         self.torch = torch
         self.lib = _abi.load_library()
@@ -204,6 +204,8 @@ class HeliVecEnv(*_VEC_BASES):
                                           self.num_envs, ctypes.byref(h)), self.lib)
         self._h = h
         self._specialized = bool(self.lib.hg_set_specialized(h, 1))
+        if specialize and not self._specialized:
+            self.specialize()
         N, dev = self.num_envs, self.device
         f32, u8, i32 = torch.float32, torch.uint8, torch.int32
         self.obs = torch.empty((N, _abi.HG_N_OBS), dtype=f32, device=dev)
@@ -429,9 +431,26 @@ class HeliVecEnv(*_VEC_BASES):
 
     @property
     def specialized(self):
-        """True when steps run a constant-specialised kernel (the default AW109 airframe's constants
-        compiled in): every step and rollout, with or without the optional features (reset info,
-        re-trim, next-step auto-reset, TimeLimit, per-env templates)."""
+        """True when steps run a constant-specialised kernel: the library's own for the default AW109
+        airframe (its constants compiled in; every step and rollout, with or without the optional
+        features), or a run-time specialised one for any other airframe (specialize())."""
+        return self._specialized
+
+    def specialize(self):
+        """Step this env with a kernel specialised for its airframe's constants (heligym_amd._rtc:
+        compiled with hipcc on the first request for these constants, ~4 s, then cached), the way the
+        default airframe always is: per-step launches with in-kernel noise use it, results bitwise
+        those of the generic kernel.  Returns whether a specialised kernel is in use."""
+        if self._specialized:
+            return True
+        from . import _rtc
+        rows, cols = self.terrain_ft.shape
+        path, img = _rtc.build(self.lib, self.cfg, rows, cols, self.cfg.task)
+        buf = ctypes.create_string_buffer(img, len(img))
+        rc = self.lib.hg_load_specialized(self._h, path.encode(), self.cfg.task, buf, len(img))
+        if rc < 0:
+            self._check(rc)
+        self._specialized = bool(rc)
         return self._specialized
 
     def set_trim_cond(self, trim_cond=None):

@@ -279,6 +279,17 @@ int32_t hg_trim_conds_batch(hg_env* env, const hg_trim_cond* conds, int64_t coun
  * template.  Copied; HG_RESET_TEMPLATE mode only. */
 int32_t hg_set_reset_templates(hg_env* env, const float* templates_dev, void* stream);
 
+/* Run-time specialisation for airframes other than the compiled-in default one (whose constants
+ * are instruction literals of the library's step kernel): load a gfx950 code object built from
+ * csrc/step_rtc.hip with this env's constant image (`image`, the sizeof(Params<float>) bytes
+ * hg_debug_params returns with baked_only = 1) for `task`.  Per-step launches (no injected noise,
+ * not hg_rollout) of an env whose constants match the image then run its kernels; results are
+ * bitwise those of the generic kernel.  Returns 1 when in use, 0 when loaded but not matching,
+ * < 0 on error.  Not part of the reference surface (replaces nothing: the reference has one
+ * NumPy code path for every airframe). */
+int32_t hg_load_specialized(hg_env* env, const char* code_object_path, int32_t task, const void* image,
+                            int64_t bytes);
+
 /* Number of RETRIM-mode auto-resets so far whose trim failed (those envs got the template state).
  * Synchronises with the device. */
 int32_t hg_retrim_failures(hg_env* env, int64_t* count);

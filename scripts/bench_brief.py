@@ -12,4 +12,13 @@ for f in sys.argv[1:]:
         if v:
             ms = v.get("ms_per_step") if v.get("ms_per_step") is not None else v.get("window_ms_per_step")
             out.append(f"  {k}: {ms * 1e3 if ms else float('nan'):.2f} us resets {v.get('resets_in_window')}")
+    af = d.get("airframes")
+    if af and "error" not in af:
+        for k, v in af.items():
+            if isinstance(v, dict):
+                out.append(f"  airframe {k}: generic {v['generic_ms_per_step']*1e3:.2f} us, specialised "
+                           f"{v['specialised_ms_per_step']*1e3:.2f} us ({v['specialised_over_default_airframe']:.3f} x default), "
+                           f"build {v['specialise_s']:.1f} s")
+    elif af:
+        out.append(f"  airframes: {af}")
     print("\n".join(out))

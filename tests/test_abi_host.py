@@ -190,3 +190,33 @@ def test_specialised_kernel_selection(lib, kw, baked):
         cfg, _ = config.make_config(**kw)
     assert lib.hg_config_is_baked(ctypes.byref(cfg), 1024, 1024) == (1 if baked else 0)
     assert lib.hg_config_is_baked(ctypes.byref(cfg), 512, 512) == 0   # other terrain size
+
+
+def test_rtc_flags_match_library_build():
+    """heligym_amd._rtc compiles the step code with the flags the library's step translation unit
+    gets (__graft_entry__.HIP_FLAGS and heligym_amd.hip's own), so its kernels round alike."""
+    import __graft_entry__ as ge
+    from heligym_amd import _rtc
+    step_flags = dict(ge.SOURCES)[ge.SRC]
+    assert _rtc.FLAGS == ge.HIP_FLAGS + step_flags
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/rocm/bin/hipcc"), reason="no hipcc")
+def test_rtc_code_object_builds(lib, tmp_path, monkeypatch):
+    """The run-time specialisation pipeline on the CPU side: another airframe's constant image,
+    compiled into a gfx950 code object holding the six per-step kernels, cached by key."""
+    from heligym_amd import _rtc
+    monkeypatch.setenv("HELIGYM_AMD_CACHE", str(tmp_path))
+    cfg, _ = config.make_config(heli_name=golden_cases.load_variant("heavy")[1])
+    assert lib.hg_config_is_baked(ctypes.byref(cfg), 1024, 1024) == 0
+    path, img = _rtc.build(lib, cfg, 1024, 1024, cfg.task)
+    assert os.path.getsize(path) > 10000 and len(img) % 4 == 0
+    blob = open(path, "rb").read()
+    for name in ("hg_rtc_step_nt", "hg_rtc_step_nt_feat", "hg_rtc_step_nts", "hg_rtc_step_nts_feat",
+                 "hg_rtc_step_bulk", "hg_rtc_step_bulk_feat"):
+        assert name.encode() in blob
+    t = os.path.getmtime(path)
+    assert _rtc.build(lib, cfg, 1024, 1024, cfg.task)[0] == path and os.path.getmtime(path) == t   # cached
+    # the image is the baked fields of this airframe, not the default one's
+    cfg0, _ = config.make_config()
+    assert _rtc.image(lib, cfg0, 1024, 1024) != img

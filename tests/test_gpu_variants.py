@@ -60,3 +60,44 @@ def test_nt_variant_equals_bulk_variant(torch):
         if f[2] is not None:
             resets += int(f[2].sum())
     assert resets > 0
+
+
+@pytest.mark.parametrize("variant", ["heavy", "wing"])
+def test_runtime_specialised_kernel_bitwise_equals_generic(torch, variant, tmp_path, monkeypatch):
+    """Another airframe (the heavier one with other rotor speeds; the winged one) stepped with its
+    run-time specialised kernel (heligym_amd._rtc: its constants compiled in) and with the generic
+    kernel: observations, rewards, flags and the final state bitwise equal over 300 steps with
+    in-kernel noise and auto-resets, in the lone-wave and bulk launch variants, with and without
+    the optional features (TimeLimit)."""
+    import golden_cases as gc
+    from heligym_amd import HeliVecEnv
+    monkeypatch.setenv("HELIGYM_AMD_CACHE", str(tmp_path))
+    doc = gc.load_variant(variant)[1]
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    for n, kw in ((4097, {}), (4097, dict(max_episode_steps=150)), (2 * 2 * 64 * 4 * cus + 65, {})):
+        outs = []
+        for spec in (False, True):
+            env = HeliVecEnv(n, task="hover", dt=0.01, heli_name=doc, seed=3, autoreset=True, device="cuda:0", **kw)
+            assert not env.specialized
+            if spec:
+                assert env.specialize() and env.specialized
+            env.reset()
+            act = torch.empty((n, 4), dtype=torch.float32, device=env.device)
+            rec = []
+            for k in range(300):
+                env.random_actions(act, seed=4, step=k)
+                act[::4, 0] = -1.0   # crashes and resets
+                env.step_async(act, with_reset_info=False)
+                if k % 50 == 49:
+                    rec.append([b.clone() for b in (env.obs, env.reward, env.terminated_u8, env.truncated_u8)])
+            st, ctr = env.get_state()
+            torch.cuda.synchronize()
+            outs.append(([[b.cpu().numpy() for b in r] for r in rec], st.cpu().numpy(), ctr.cpu().numpy()))
+            env.close()
+        done = sum(int(r[2].sum() + r[3].sum()) for r in outs[0][0])
+        assert done > 0
+        for ra, rb in zip(outs[0][0], outs[1][0]):
+            for x, y in zip(ra, rb):
+                np.testing.assert_array_equal(x.view(np.uint8), y.view(np.uint8))
+        np.testing.assert_array_equal(outs[0][1].view(np.int32), outs[1][1].view(np.int32))
+        np.testing.assert_array_equal(outs[0][2], outs[1][2])
