@@ -745,26 +745,33 @@ def main():
         if world == 1 and not args.no_secondary and not args.dry_run and args.reset_mode == "template":
             # the same workload with exact F8 resets: every auto-reset re-trimmed on the device against
             # the env's last wind (reset_mode="retrim", helicopter.py:208-212)
-            envr = make_env(argparse.Namespace(**{**vars(args), "reset_mode": "retrim"}), torch, N, rank * N, dev)
             Kr = min(K, 500)
+            for name, mode in (("retrim", args.autoreset_mode), ("retrim_next_step", "next_step")):
+                if name == "retrim_next_step" and args.autoreset_mode == "next_step":
+                    continue
+                envr = make_env(argparse.Namespace(**{**vars(args), "reset_mode": "retrim", "autoreset_mode": mode}),
+                                torch, N, rank * N, dev)
 
-            def stepr(k):
-                envr.step_async(bank[k % B], with_reset_info=False)
-            aged_r = age(args, torch, envr, bank, B)
-            for k in range(min(args.warmup, 50)):
-                stepr(k)
-            repr_, _kr = graphs_for(torch, dev, stepr, Kr, B)
-            s_rt, _, _, rs_rt = timer.run_counted(envr, repr_, 3)
-            del _kr
-            # a window without a reset would time the plain step, not the re-trim: no value then
-            secondary["retrim"] = {
-                "envs": N, "value": N * Kr / s_rt if rs_rt > 0 else None, "unit": "env-steps/s",
-                "ms_per_step": s_rt / Kr * 1e3 if rs_rt > 0 else None, "window_ms_per_step": s_rt / Kr * 1e3,
-                "resets_in_window": rs_rt, "aged_steps": aged_r,
-                "steps": Kr, "retrim_failures": envr.retrim_failures(),
-                "note": "reset_mode='retrim': each step's auto-resets re-trimmed on the device (Newton trim "
-                        "against the env's last wind, the reference's reset from episode 2 on), hipGraph"}
-            envr.close()
+                def stepr(k):
+                    envr.step_async(bank[k % B], with_reset_info=False)
+                aged_r = age(args, torch, envr, bank, B)
+                for k in range(min(args.warmup, 50)):
+                    stepr(k)
+                repr_, _kr = graphs_for(torch, dev, stepr, Kr, B)
+                s_rt, _, _, rs_rt = timer.run_counted(envr, repr_, 3)
+                del _kr
+                ov = mode == "next_step" and envr.set_retrim_overlap(True)
+                # a window without a reset would time the plain step, not the re-trim: no value then
+                secondary[name] = {
+                    "envs": N, "value": N * Kr / s_rt if rs_rt > 0 else None, "unit": "env-steps/s",
+                    "ms_per_step": s_rt / Kr * 1e3 if rs_rt > 0 else None, "window_ms_per_step": s_rt / Kr * 1e3,
+                    "resets_in_window": rs_rt, "aged_steps": aged_r, "autoreset_mode": mode,
+                    "steps": Kr, "retrim_failures": envr.retrim_failures(),
+                    "note": "reset_mode='retrim': each auto-reset re-trimmed on the device (Newton trim against the "
+                            "env's last wind, the reference's reset from episode 2 on), hipGraph"
+                            + ("; next-step auto-reset (make_vec's configuration): the episodes a step ends are "
+                               "trimmed on side streams while the next step runs" if ov else "")}
+                envr.close()
 
         if world == 1 and not args.no_secondary and not args.dry_run and args.envs < OUT_OF_CACHE_ENVS:
             # the same step past the 256 MB Infinity Cache (1.32 GB moved per launch): HBM bytes, not

@@ -117,6 +117,13 @@ struct StepArgs {
     int4* retrim_recs;       // ... compacted jobs {env, trim wind} of the envs to re-trim
     int32_t* retrim_count;   // ... their number: retrim_count[max(retrim_slot, 0)]
     const float* tmpl_env;   // per-env reset templates [N][39] (Params::env_templates), else unused
+    // next-step auto-resets re-trimmed concurrently with the following step (reset_mode RETRIM):
+    int4* ov_recs;           // jobs {env, trim wind} of the envs whose episode ends this step, or NULL
+    int32_t* ov_count;       // ... their number (zeroed by the previous step of the sequence)
+    int32_t* ov_count_next;  // ... the next step's count, zeroed by this launch
+    int32_t ov_active;       // the resets due this step are being trimmed by a concurrent retrim_kernel
+                             // (ov mode): their state, but for the step counter, and their observation
+                             // rows are that kernel's to write
 };
 
 // Model constants travel as a pointer to a device copy (scalar loads); by value they would take
@@ -195,15 +202,21 @@ __device__ __forceinline__ void st_lane(T* base, uint32_t idx, T v) {
 // bank-conflict free) and writes them back as contiguous float4, with no block-wide barrier.
 // MULTI (hg_rollout): step s's rows start at obs + s*N*17 floats, 16-byte aligned only when
 // N % 4 == 0 (or s % 4 == 0); unaligned rows go out as dwords.
+// `skip` (uniform): rows another kernel writes (the concurrently re-trimmed resets), stored around.
 template <bool NT, bool MULTI>
 __device__ __forceinline__ void store_obs_wave(float* w_obs, const float obs[17], float* dst, int64_t so, int64_t w0,
-                                               int64_t n, int lane) {
+                                               int64_t n, int lane, uint64_t skip = 0) {
 #pragma unroll
     for (int c = 0; c < 17; ++c) w_obs[lane * 17 + c] = obs[c];
     __builtin_amdgcn_wave_barrier();
     const int nw = (n - w0) < 64 ? (int)(n - w0) : 64;
     const int cnt = nw > 0 ? nw * 17 : 0;
     float* out = dst + (so + w0) * 17;
+    if (skip) {
+        for (int j = lane; j < cnt; j += 64)
+            if (!((skip >> (j / 17)) & 1)) st_out<NT>(out + j, w_obs[j]);
+        return;
+    }
     const bool aligned = !MULTI || (((uintptr_t)out & 15) == 0);
     if (nw == 64 && aligned) {   // full wave: 272 float4, all LDS reads issued before the first store
         f32x4 v[5];
@@ -394,8 +407,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     if (FEAT && blockIdx.x == 0 && tid == 0) {   // counters of a later step (rings of three)
         if (a.reset_count_next) *a.reset_count_next = 0;
         if (a.retrim_slot >= 0 && a.retrim_count) a.retrim_count[a.retrim_slot == 2 ? 0 : a.retrim_slot + 1] = 0;
+        if (a.ov_count_next) *a.ov_count_next = 0;
     }
     const int nsteps = MULTI ? a.nsteps : 1;
+    bool defer_st = false;   // (one step per launch) a deferred reset: the step counter alone is stored
     for (int sstep = 0; sstep < nsteps; ++sstep) {
     // MULTI: the constants are re-read (scalar cache) each step rather than kept live across the
     // loop, where ~130 of them would spill out of the SGPR file
@@ -482,6 +497,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
 
     // auto-reset (same step, or the step after the end)
     const bool do_reset = P.autoreset && active && ((FEAT && P.autoreset_next) ? pending : done);
+    // a next-step reset whose trim runs concurrently with this step (ov mode): only the step counter
+    // is stored here
+    const bool defer = FEAT && a.ov_active && do_reset;
+    defer_st = defer;
     if (active) {
         st_lane<kNTS>(a.reward + so + blk0, (uint32_t)tid, pending ? 0.f : rew);
         st_lane<kNTS>(a.terminated + so + blk0, (uint32_t)tid, (uint8_t)term);
@@ -518,15 +537,28 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
             }
         }
     }
+    if (FEAT && a.ov_recs) {   // ov mode: the episodes ending now, trimmed while the next step runs
+        const bool ends = active && done && P.autoreset;
+        const unsigned long long mask = __ballot(ends);
+        if (mask) {
+            const int leader = __ffsll((long long)mask) - 1;
+            int base = 0;
+            if (lane == leader) base = atomicAdd(a.ov_count, __popcll(mask));
+            base = __shfl(base, leader);
+            const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
+            if (ends && slot < n)
+                a.ov_recs[slot] = make_int4((int32_t)i, __float_as_int(W[0]), __float_as_int(W[1]), __float_as_int(W[2]));
+        }
+    }
     if (FEAT && P.reset_retrim) {   // queue the resets for retrim_kernel (which overwrites the template)
-        const unsigned long long mask = __ballot(do_reset);
+        const unsigned long long mask = __ballot(do_reset && !defer);
         if (mask) {
             const int leader = __ffsll((long long)mask) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(a.retrim_count + (a.retrim_slot > 0 ? a.retrim_slot : 0), __popcll(mask));
             base = __shfl(base, leader);
             const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
-            if (do_reset && slot < n) {
+            if (do_reset && !defer && slot < n) {
                 // the job carries its trim wind: this step's (same-step reset), or the one recorded at
                 // the episode's last step (next-step reset)
                 float w0 = W[0], w1 = W[1], w2 = W[2];
@@ -584,12 +616,17 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
         carry[3] = obs[16];
         if (FEAT && P.autoreset_next && done) step = -step - 1;   // reset on the next step (n = step kept)
     }
-    store_obs_wave<kNTS, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, a.obs, so, blk0, n, lane);
+    uint64_t skip_rows = 0;
+    if (FEAT && !MULTI) skip_rows = __ballot(defer);
+    store_obs_wave<kNTS, MULTI>(s_obs + wv * 64 * HG_N_OBS, obs, a.obs, so, blk0, n, lane, skip_rows);
     }   // steps
     TSTAMP(13, "v"(hs[0]), "v"(carry[3]));
     st_b = reinterpret_cast<f32x4*>(state_p + tile * kTileWords) + 4 * kTileEnvs;
     asm volatile("" : "+s"(st_b));
-    if (active) {
+    if (FEAT && !MULTI && __ballot(defer_st)) {   // a deferred reset: its step counter only (the trim writes the rest)
+        if (defer_st) reinterpret_cast<int32_t*>(GRP(st_b, 0) + tid)[3] = 0;
+    }
+    if (active && !(FEAT && !MULTI && defer_st)) {
         // the lane index re-materialised in this block, so that each store selects the SGPR-base
         // form (a 32-bit lane offset) instead of a 64-bit VALU address add per store
         uint32_t t = (uint32_t)tid;
@@ -1097,6 +1134,21 @@ struct hg_env {
     int32_t* retrim_ring = nullptr;         // [3] jobs of a step's re-trim: step k counts into [k % 3] and
     uint64_t retrim_gen = 0;                //     zeroes [(k + 1) % 3] from its kernel (no memset launch)
     uint64_t retrim_chain = kChainBroken;   // chain key of the previous re-trim step (see chain_key)
+    // ov mode (reset_mode RETRIM with next-step auto-reset): the episodes a step ends are re-trimmed on a
+    // side stream while the next step runs.  Step k queues its ends into ov_recs[k % 3] / ov_ring[k % 3];
+    // step k+1's call forks their trim (after step k) onto ov_side[k % 2], launches step k+1 -- which
+    // stores only the step counter of those envs -- and joins the trim back before returning, so the
+    // caller's stream sees step k+1 complete.  Consecutive trims overlap each other too (one side stream
+    // each), and every step waits only for the trim of the ends of the step before the previous one.
+    bool ov = false;                        // configured (RETRIM + next-step auto-reset) and enabled
+    bool ov_enabled = true;                 // hg_set_retrim_overlap
+    uint64_t ov_chain = kChainBroken;       // chain key of the previous step when its ends can be trimmed
+                                            // concurrently with this one (no other call in between)
+    int4* ov_recs = nullptr;                // [3][N] jobs {env, trim wind}
+    int32_t* ov_ring = nullptr;             // [3] their counts
+    hipStream_t ov_side[2] = {nullptr, nullptr};
+    hipEvent_t ov_fork[3] = {nullptr, nullptr, nullptr};   // after step k's launch: its trim may start
+    hipEvent_t ov_join[2] = {nullptr, nullptr};            // a side stream's trim is done
     float* tmpl_env = nullptr;              // per-env reset templates [N][39] (hg_set_reset_templates)
     bool env_templates = false;
     bool baked = false;                     // step with the constant-specialised kernel (baked.h)
@@ -1166,6 +1218,7 @@ static hipError_t reanchor_azimuths(hg_env* e) {
 }
 
 static int32_t build_template(hg_env* e) {
+    e->ov_chain = kChainBroken;   // the next step's pending resets take the serial re-trim
     const double W[3] = {e->Pd.wm[0], e->Pd.wm[1], e->Pd.wm[2]};   // helicopter.py:55 (mean wind)
     hg_trim_result r;
     memset(&r, 0, sizeof(r));
@@ -1358,6 +1411,22 @@ static std::vector<float2> split_terrain(const double* t, int32_t rows, int32_t 
     return v;
 }
 
+// every device resource of a handle (create's error paths and hg_destroy), then the handle
+static void release(hg_env* e) {
+    if (e->rtc_mod) (void)hipModuleUnload(e->rtc_mod);
+    dfree(e->hmap); dfree(e->state); dfree(e->az); dfree(e->tmpl_dev); dfree(e->params_dev);
+    dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_recs);
+    dfree(e->retrim_count); dfree(e->retrim_ring); dfree(e->ov_recs); dfree(e->ov_ring);
+    dfree(e->tmpl_env); dfree(e->setup_batch);
+    for (hipStream_t& q : e->ov_side)
+        if (q) (void)hipStreamDestroy(q);
+    for (hipEvent_t& v : e->ov_fork)
+        if (v) (void)hipEventDestroy(v);
+    for (hipEvent_t& v : e->ov_join)
+        if (v) (void)hipEventDestroy(v);
+    delete e;
+}
+
 int32_t hg_trim(const hg_config* cfg, const double* terrain_ft, int32_t rows, int32_t cols,
                 const double wind_ned[3], hg_trim_result* out) {
     int32_t rc = check_config(cfg, rows, cols);
@@ -1390,11 +1459,7 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     rc = build_template(e);
     if (rc != HG_OK) { delete e; return rc; }
     auto cleanup = [&](hipError_t err, const char* what) {
-        dfree(e->hmap); dfree(e->state); dfree(e->az); dfree(e->tmpl_dev); dfree(e->params_dev);
-        dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_recs); dfree(e->retrim_count);
-        dfree(e->retrim_ring);
-        dfree(e->tmpl_env); dfree(e->setup_batch);
-        delete e;
+        release(e);
         return fail(HG_E_HIP, std::string(what) + ": " + hipGetErrorString(err));
     };
     hipError_t err;
@@ -1436,6 +1501,23 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
         hipLaunchKernelGGL(fill_wind_kernel, dim3(grid_for(num_envs)), dim3(kBlock), 0, 0, e->retrim_wind, num_envs,
                            (float)e->Pd.wm[0], (float)e->Pd.wm[1], (float)e->Pd.wm[2]);
         if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "fill_wind_kernel");
+
+        if (cfg->autoreset && cfg->autoreset_mode == HG_AUTORESET_NEXT_STEP) {   // ov mode's buffers, streams, events
+            if ((err = hipMalloc(&e->ov_recs, sizeof(int4) * 3 * num_envs)) != hipSuccess)
+                return cleanup(err, "hipMalloc ov jobs");
+            if ((err = hipMalloc(&e->ov_ring, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc ov ring");
+            if ((err = hipMemset(e->ov_ring, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset ov ring");
+            for (hipStream_t& q : e->ov_side)
+                if ((err = hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != hipSuccess)
+                    return cleanup(err, "hipStreamCreate ov");
+            for (hipEvent_t& v : e->ov_fork)
+                if ((err = hipEventCreateWithFlags(&v, hipEventDisableTiming)) != hipSuccess)
+                    return cleanup(err, "hipEventCreate ov");
+            for (hipEvent_t& v : e->ov_join)
+                if ((err = hipEventCreateWithFlags(&v, hipEventDisableTiming)) != hipSuccess)
+                    return cleanup(err, "hipEventCreate ov");
+            e->ov = true;
+        }
     }
     const int64_t slots = hgk::tile_words(num_envs) / hgk::kEnvSlots;
     hipLaunchKernelGGL(init_kernel, dim3(grid_for(slots)), dim3(kBlock), 0, 0, e->tmpl, e->state, slots, e->az,
@@ -1449,22 +1531,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
 void hg_destroy(hg_env* e) {
     if (!e) return;
     DevGuard dev_guard(e);
-    if (e->rtc_mod) (void)hipModuleUnload(e->rtc_mod);
-    dfree(e->hmap);
-    dfree(e->state);
-    dfree(e->az);
-    dfree(e->tmpl_dev);
-    dfree(e->params_dev);
-    dfree(e->setup_dev);
-    dfree(e->pd_dev);
-    dfree(e->retrim_wind);
-    dfree(e->retrim_list);
-    dfree(e->retrim_recs);
-    dfree(e->retrim_count);
-    dfree(e->retrim_ring);
-    dfree(e->tmpl_env);
-    dfree(e->setup_batch);
-    delete e;
+    if (e->ov) (void)hipDeviceSynchronize();   // trims queued on the side streams
+    release(e);
 }
 
 int64_t hg_num_envs(const hg_env* e) { return e ? e->n : -1; }
@@ -1540,6 +1608,7 @@ int32_t hg_get_template(const hg_env* e, hg_trim_result* out) {
 
 int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    e->ov_chain = kChainBroken;   // the next step's pending resets take the serial re-trim
     DevGuard dev_guard(e);
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     hipStream_t s = (hipStream_t)stream;
@@ -1604,12 +1673,43 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     if (zero_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
     int32_t* rt_count = nullptr;
     int32_t rt_slot = -1;
+    const bool ov = retrim && e->ov && e->ov_enabled;
+    // ov mode: the previous step's ends are trimmed concurrently with this step when it was this
+    // sequence's previous launch (no other call in between; not across captures or from an eager step
+    // after a capture, whose graphs may have run in between)
+    const bool ov_active = ov && e->ov_chain == key && !eager_after_capture;
+    int ov_side = -1;
     if (retrim) {   // the step's re-trim job count: a slot of the ring, zeroed by the previous step's kernel
         rt_slot = (int32_t)(e->retrim_gen % 3);
         rt_count = e->retrim_ring + rt_slot;
+        ov_side = (int)((e->retrim_gen + 1) & 1);   // = (k - 1) & 1 for the trim of step k - 1's ends
         ++e->retrim_gen;
-        if (e->retrim_chain != key || eager_after_capture) HIP_TRY(hipMemsetAsync(rt_count, 0, sizeof(int32_t), s));
+        if (e->retrim_chain != key || eager_after_capture) {
+            HIP_TRY(hipMemsetAsync(rt_count, 0, sizeof(int32_t), s));
+            if (ov) HIP_TRY(hipMemsetAsync(e->ov_ring + rt_slot, 0, sizeof(int32_t), s));
+        }
         e->retrim_chain = key;
+    }
+    if (ov_active) {   // the previous step's ends: trimmed on a side stream, concurrently with this step
+        const int prev = rt_slot == 0 ? 2 : rt_slot - 1;
+        hipStream_t side = e->ov_side[ov_side];
+        HIP_TRY(hipStreamWaitEvent(side, e->ov_fork[prev], 0));
+        hgk::RetrimArgs r;
+        memset(&r, 0, sizeof(r));
+        r.P = e->pd_dev;
+        r.T = e->setup_dev;
+        r.count = e->ov_ring + prev;
+        r.recs = e->ov_recs + (int64_t)prev * e->n;
+        r.state = e->state;
+        r.az = e->az;
+        r.obs = obs;
+        r.n = e->n;
+        r.fail_count = e->retrim_count + 1;
+        r.ov = 1;
+        r.tmpl = reinterpret_cast<const float*>(e->tmpl_dev);
+        r.tmpl_env = e->Pf.env_templates ? e->tmpl_env : nullptr;
+        HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), side));
+        HIP_TRY(hipEventRecord(e->ov_join[ov_side], side));
     }
     StepArgs a;
     a.hmap = e->hmap;
@@ -1631,11 +1731,20 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.retrim_slot = rt_slot;
     a.tmpl_env = e->tmpl_env;
     a.nsteps = 1;
+    a.ov_recs = ov ? e->ov_recs + (int64_t)rt_slot * e->n : nullptr;
+    a.ov_count = ov ? e->ov_ring + rt_slot : nullptr;
+    a.ov_count_next = ov ? e->ov_ring + (rt_slot == 2 ? 0 : rt_slot + 1) : nullptr;
+    a.ov_active = ov_active ? 1 : 0;
     const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next ||
                       e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
     dispatch_task<false>(e, s, a, eta != nullptr, feat);
     HIP_TRY(hipGetLastError());
-    if (retrim) {   // re-trim this step's resets against their last wind (overwrites the template)
+    if (ov) {
+        HIP_TRY(hipEventRecord(e->ov_fork[rt_slot], s));   // this step's ends may be trimmed from here on
+        if (ov_active) HIP_TRY(hipStreamWaitEvent(s, e->ov_join[ov_side], 0));
+        e->ov_chain = key;
+    }
+    if (retrim && !ov_active) {   // re-trim this step's resets against their last wind (overwrites the template)
         hgk::RetrimArgs r;
         memset(&r, 0, sizeof(r));
         r.P = e->pd_dev;
@@ -1677,6 +1786,7 @@ int32_t hg_step_rows(hg_env* e, const float* actions, float* obs, float* reward,
 int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, float* reward, uint8_t* terminated,
                    uint8_t* truncated, uint8_t* info, const float* eta, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    e->ov_chain = kChainBroken;   // the next step's pending resets take the serial re-trim
     DevGuard dev_guard(e);
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (nsteps < 1) return fail(HG_E_INVALID, "nsteps must be >= 1");
@@ -1770,6 +1880,7 @@ int32_t hg_trim_conds_batch(hg_env* e, const hg_trim_cond* conds, int64_t count,
 
 int32_t hg_set_reset_templates(hg_env* e, const float* templates, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    e->ov_chain = kChainBroken;   // the next step's pending resets take the serial re-trim
     DevGuard dev_guard(e);
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (templates && e->cfg.reset_mode == HG_RESET_RETRIM)
@@ -1797,6 +1908,13 @@ int32_t hg_retrim_failures(hg_env* e, int64_t* count) {
     return HG_OK;
 }
 
+int32_t hg_set_retrim_overlap(hg_env* e, int32_t enable) {
+    if (!e) return fail(HG_E_INVALID, "env is NULL");
+    e->ov_enabled = enable != 0;
+    e->ov_chain = kChainBroken;
+    return (e->ov && e->ov_enabled) ? 1 : 0;
+}
+
 int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     DevGuard dev_guard(e);
@@ -1811,6 +1929,7 @@ int32_t hg_get_state(hg_env* e, float* state, int32_t* counters, void* stream) {
 
 int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, void* stream) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    e->ov_chain = kChainBroken;   // the next step's pending resets take the serial re-trim
     DevGuard dev_guard(e);
     if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
     if (!state && !counters) return HG_OK;

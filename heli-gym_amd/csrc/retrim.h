@@ -72,6 +72,12 @@ struct RetrimArgs {
     float* out_obs;
     int32_t* out_status;
     int32_t* fail_count;    // env mode: trims that failed (env keeps the template reset)
+    // ov mode (env mode, jobs from recs): the next-step resets of envs whose step runs concurrently.
+    // That step stores only their step counter, so the trim writes the whole reset -- the wind
+    // states and success counter zeroed, the episode index advanced -- and on failure the template.
+    int32_t ov;
+    const float* tmpl;      // ov: the shared reset template (heli 18 | carry 4 | obs 17) ...
+    const float* tmpl_env;  // ... or the per-env ones [N][39] (Params::env_templates), else NULL
 };
 
 // Launch retrim_kernel (one 64-lane block per trim, up to `grid` blocks looping over the jobs).

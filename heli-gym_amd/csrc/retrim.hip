@@ -205,7 +205,14 @@ __device__ __forceinline__ void retrim_write(const RetrimArgs& a, const hg::Para
     if (a.list || a.recs) {
         for (int c = 0; c < 18; ++c)
             if (has_slot(c)) a.state[tix(env, c)] = (float)s[c];
-        const int32_t epi = reinterpret_cast<const int32_t*>(a.state)[tix(env, kCtrCol0 + 2)];
+        int32_t* ctr = reinterpret_cast<int32_t*>(a.state);
+        int32_t epi = ctr[tix(env, kCtrCol0 + 2)];
+        if (a.ov) {   // the rest of the reset (the concurrent step stored the step counter)
+            epi += 1;
+            for (int c = 18; c < 23; ++c) a.state[tix(env, c)] = 0.f;
+            ctr[tix(env, kCtrCol0 + 1)] = 0;
+            ctr[tix(env, kCtrCol0 + 2)] = epi;
+        }
         a.az[env] = AzRec{(float)s[kAzCol0], (float)s[kAzCol0 + 1], 0, epi};   // the reset's step 0
         const int co[4] = {4, 5, 6, 16};
         for (int c = 0; c < 4; ++c) a.state[tix(env, 23 + c)] = (float)ob[co[c]];
@@ -220,6 +227,24 @@ __device__ __forceinline__ void retrim_write(const RetrimArgs& a, const hg::Para
             for (int c = 0; c < 17; ++c) a.out_obs[job * 17 + c] = (float)ob[c];
     }
     if (a.out_status) a.out_status[job] = HG_OK;
+}
+
+// ov mode, a failed trim: the env takes the template reset the step would have stored (the
+// reference raises instead, helicopter_dynamics.py:543-544; the failure is counted)
+__device__ __forceinline__ void retrim_write_template(const RetrimArgs& a, int64_t env) {
+    const float* tr = a.tmpl_env ? a.tmpl_env + env * 39 : a.tmpl;
+    for (int c = 0; c < 18; ++c)
+        if (has_slot(c)) a.state[tix(env, c)] = tr[c];
+    for (int c = 18; c < 23; ++c) a.state[tix(env, c)] = 0.f;
+    for (int c = 0; c < 4; ++c) a.state[tix(env, 23 + c)] = tr[18 + c];
+    int32_t* ctr = reinterpret_cast<int32_t*>(a.state);
+    const int32_t epi = ctr[tix(env, kCtrCol0 + 2)] + 1;
+    ctr[tix(env, kCtrCol0 + 1)] = 0;
+    ctr[tix(env, kCtrCol0 + 2)] = epi;
+    // an episode begun from the template: the azimuth record anchors the template's azimuths
+    a.az[env] = AzRec{tr[kAzCol0], tr[kAzCol0 + 1], 0, epi};
+    if (a.obs)
+        for (int c = 0; c < 17; ++c) a.obs[env * 17 + c] = tr[22 + c];
 }
 
 // One wave per trim.  Each evaluation round evaluates 42 points at once: lanes 0..31 the +-eps
@@ -398,6 +423,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WA
                 retrim_write(a, P, T, job, env, x, e);
             }
         } else if (l == 0) {
+            if (a.ov) retrim_write_template(a, env);
             if (a.fail_count) atomicAdd(a.fail_count, 1);
             if (a.out_status) a.out_status[job] = HG_E_TRIM;
         }

@@ -429,6 +429,15 @@ class HeliVecEnv(*_VEC_BASES):
         self._specialized = bool(rc)
         return self._specialized
 
+    def set_retrim_overlap(self, enable=True):
+        """reset_mode="retrim" with next-step auto-reset: trim the episodes a step ends while the next
+        step runs (hg_set_retrim_overlap; the default, bitwise the serial results).  Returns whether
+        the overlap is in effect."""
+        rc = self.lib.hg_set_retrim_overlap(self._h, 1 if enable else 0)
+        if rc < 0:
+            self._check(rc)
+        return bool(rc)
+
     @property
     def specialized(self):
         """True when steps run a constant-specialised kernel: the library's own for the default AW109

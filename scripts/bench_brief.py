@@ -7,7 +7,7 @@ for f in sys.argv[1:]:
     t = d.get("timing", {})
     out = [f"{f}: K={d['steps']} head {d['ms_per_step'] * 1e3:.3f} us (resets/window {t.get('resets_in_window')}, "
            f"aged {t.get('aged_steps')}) frac {d['roofline']['frac']:.3f}"]
-    for k in ("step_with_reset_info", "step_api_eager", "generic_kernel", "rollout", "retrim", "out_of_cache"):
+    for k in ("step_with_reset_info", "step_api_eager", "generic_kernel", "rollout", "retrim", "retrim_next_step", "out_of_cache"):
         v = d.get(k)
         if v:
             ms = v.get("ms_per_step") if v.get("ms_per_step") is not None else v.get("window_ms_per_step")

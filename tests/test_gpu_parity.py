@@ -840,6 +840,83 @@ def test_next_step_autoreset(torch):
     assert checked > N // 2, checked
 
 
+def _retrim_next_step_run(torch, N, K, overlap, graph_steps=0, seed=13):
+    """reset_mode="retrim" + next-step auto-reset, half the envs crashing (low collective): per-step
+    obs, reward, flags and info, plus the state and counters read mid-run and at the end.  Eager, a
+    get_state() at step 100 and a masked reset() at step 150 (each breaks the overlap chain once); or,
+    with graph_steps, hipGraphs of that many steps (each recording its outputs) replayed back to back
+    with one eager step between two replays."""
+    env = make_env(torch, N, "hover", 0.02, autoreset=True, reset_mode="retrim", autoreset_mode="next_step",
+                   seed=seed)
+    assert env.set_retrim_overlap(overlap) == overlap
+    env.reset()
+    acts = torch.empty((K, N, 4), dtype=torch.float32, device=env.device)
+    for k in range(K):
+        env.random_actions(acts[k], seed=4, step=k)
+    acts[:, : N // 2, 0] = -1.0
+    bufs = [torch.zeros((K,) + tuple(b.shape), dtype=b.dtype, device=env.device)
+            for b in (env.obs, env.reward, env.terminated_u8, env.truncated_u8)]
+    mid = None
+
+    def one(k):
+        env.step_async(acts[k], with_reset_info=False)
+        for out, b in zip(bufs, (env.obs, env.reward, env.terminated_u8, env.truncated_u8)):
+            out[k].copy_(b)
+
+    if not graph_steps:
+        mask = torch.zeros((N,), dtype=torch.uint8, device=env.device)
+        mask[::7] = 1
+        for k in range(K):
+            one(k)
+            if k == 100:
+                mid = [x.clone() for x in env.get_state()]
+            if k == 150:
+                env.reset(mask=mask)
+    else:
+        G = graph_steps
+        s = torch.cuda.Stream(device=env.device)
+        s.wait_stream(torch.cuda.current_stream(env.device))
+        graphs = []
+        k = 0
+        while k + G <= K:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for j in range(k, k + G):
+                    one(j)
+            graphs.append((k, g))
+            k += G
+        torch.cuda.synchronize()
+        for idx, (k0, g) in enumerate(graphs):
+            g.replay()
+            if idx == 1:
+                mid = [x.clone() for x in env.get_state()]
+        for j in range(k, K):   # eager tail after the replays
+            one(j)
+    st, ctr = env.get_state()
+    torch.cuda.synchronize()
+    res = [b.cpu().numpy() for b in bufs] + [x.cpu().numpy() for x in mid] + [st.cpu().numpy(), ctr.cpu().numpy()]
+    fails = env.retrim_failures()
+    env.close()
+    return res, fails
+
+
+@pytest.mark.parametrize("graph_steps", [0, 40])
+def test_retrim_overlap_bitwise_equals_serial(torch, graph_steps):
+    """reset_mode="retrim" with next-step auto-reset (make_vec's default): the episodes a step ends
+    are re-trimmed on side streams while the next step runs (hg_set_retrim_overlap), and the results
+    -- observations, rewards, flags, state, counters -- are bitwise those of the serial path, eager
+    (with a get_state and a masked reset between steps) and graph-replayed (each graph's first step
+    takes the serial path, the others overlap)."""
+    N, K = 1000, 250 if not graph_steps else 243
+    serial, f0 = _retrim_next_step_run(torch, N, K, False, graph_steps)
+    over, f1 = _retrim_next_step_run(torch, N, K, True, graph_steps)
+    ends = int((serial[2] | serial[3]).sum())
+    assert ends > 300, ends   # re-trimmed resets happened, and many of them overlapped
+    assert f0 == f1
+    for j, (x, y) in enumerate(zip(serial, over)):
+        np.testing.assert_array_equal(x, y, err_msg=f"output {j}")
+
+
 def test_make_vec_registry_defaults(torch):
     import heligym_amd
     env = heligym_amd.make_vec("HeliHover-v0", 64, dt=0.02)
