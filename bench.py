@@ -283,7 +283,7 @@ class Timer:
             t.cuda.synchronize()
             e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
             if preroll:
-                body()
+                getattr(body, "preroll", body)()
             n0 = episodes(env, sync=False) if env is not None else None
             w0 = time.perf_counter()
             e0.record(s)
@@ -323,35 +323,34 @@ class Timer:
 
 
 def graphs_for(torch, dev, one_step, K, B):
-    """hipGraphs replaying exactly K steps: K // B captures of B steps and one of the remainder."""
+    """Exactly K steps: K // B replays of a hipGraph of B steps, then the K mod B remaining steps
+    launched eagerly.  A graph launch costs the GPU about 8 us more than the same steps launched
+    eagerly behind queued work (scripts/r04_window_probe.py: 20 steps 8.2 us per step as one graph,
+    7.85 eager, 7.83 in graphs of 100), so a remainder -- the whole window when K < B -- goes out
+    eagerly.  `replay.preroll` is one graph of B steps: the timer queues it before each window, so
+    the GPU is busy when the window starts and the host has queued the window's launches by the time
+    the GPU reaches them."""
     s = torch.cuda.Stream(device=dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     with torch.cuda.stream(s):
-        for k in range(min(B, K)):   # warm the capture stream
+        for k in range(B):   # warm the capture stream
             one_step(k)
     torch.cuda.current_stream(dev).wait_stream(s)
     torch.cuda.synchronize()
-    full = None
-    if K >= B:
-        full = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(full):
-            for k in range(B):
-                one_step(k)
-    rest = None
-    if K % B:
-        rest = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(rest):
-            for k in range(K % B):
-                one_step(k)
+    full = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(full):
+        for k in range(B):
+            one_step(k)
 
     def replay():
         for _ in range(K // B):
             full.replay()
-        if rest is not None:
-            rest.replay()
+        for k in range(K % B):
+            one_step(k)
+    replay.preroll = full.replay
     replay()
     torch.cuda.synchronize()
-    return replay, (full, rest)
+    return replay, (full,)
 
 
 class _DryEnv:
@@ -677,7 +676,8 @@ def main():
             replay, _keep = graphs_for(torch, dev, one_step, K, B)
         sec, secs, wall, resets = timer.run_counted(env, replay, R)
         per_rank = timer.per_rank
-        mode = f"hipGraphs of {B} steps"
+        mode = (f"hipGraphs of {B} steps" + (f" + {K % B} eager launches" if K % B else "") if K >= B
+                else f"{K} eager launches behind a queued {B}-step hipGraph")
         total_envs = N * world
 
         if not args.no_secondary and not args.dry_run:

@@ -26,6 +26,7 @@
 #include "physics.h"
 #include "trim.h"
 #include "retrim.h"
+#include "retrim_body.h"
 #include "baked.h"
 
 using hg::Params;
@@ -349,7 +350,8 @@ namespace {
 // the same code in kernels of their own names.
 template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool NTS>
 __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p,
-                                          ParamArg Pa, const Template<float>* __restrict__ Tp, const StepArgs& a) {
+                                          ParamArg Pa, const Template<float>* __restrict__ Tp, const StepArgs& a,
+                                          int64_t bid) {
     __shared__ float s_obs[kStepBlock * HG_N_OBS];   // one 64-row slice per wave
     constexpr bool kNTS = NT || NTS;   // non-temporal output stores
     const Params<float>& P0 = *Pa;   // model constants: scalar loads from a device copy
@@ -359,7 +361,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     if constexpr (BAKED) PB = hg::bake(*Pa);
     const int lane = threadIdx.x & 63;
     const int wv = kStepBlock == 64 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
-    const int64_t tile = (int64_t)blockIdx.x * (kStepBlock / 64) + wv;
+    const int64_t tile = bid * (kStepBlock / 64) + wv;
     const int64_t blk0 = tile * 64;   // this wave's first env
     const int tid = lane;
     const int64_t i = blk0 + tid;
@@ -404,7 +406,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
         hs[10] = g6.x; hs[11] = g6.y; hs[12] = g6.z; hs[13] = g6.w;
         hs[2] = 0.f; hs[3] = 0.f;
     }
-    if (FEAT && blockIdx.x == 0 && tid == 0) {   // counters of a later step (rings of three)
+    if (FEAT && bid == 0 && tid == 0) {   // counters of a later step (rings of three)
         if (a.reset_count_next) *a.reset_count_next = 0;
         if (a.retrim_slot >= 0 && a.retrim_count) a.retrim_count[a.retrim_slot == 2 ? 0 : a.retrim_slot + 1] = 0;
         if (a.ov_count_next) *a.ov_count_next = 0;
@@ -653,8 +655,28 @@ template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool N
 __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void step_kernel(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p,
                                                       int64_t envoff_p, ParamArg Pa,
                                                       const Template<float>* __restrict__ Tp, const StepArgs a) {
-    step_body<TASK, ETA, NT, FEAT, MULTI, BAKED, NTS>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a);
+    step_body<TASK, ETA, NT, FEAT, MULTI, BAKED, NTS>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a, blockIdx.x);
 }
+
+#ifndef HG_RTC
+// reset_mode RETRIM with next-step auto-reset (hg_env::ov): one launch holds the trims of the previous
+// step's ends -- its first `tb` blocks, one wave per trim (retrim_body.h) -- and this step, whose
+// deferred resets store only their step counter while those trims write the rest.  Both parts fit
+// two waves per SIMD (<= 256 VGPRs), so at one step wave per SIMD a trim wave shares a SIMD with a
+// step wave; the trims, dispatched first, are the long pole.  One queue and no cross-stream events:
+// dependent work on another queue waits about 10 us per hop on MI355X (profiles/r04_ov_trace.txt).
+template <int TASK, bool BAKED>
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2))) void step_ov_kernel(
+    float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p, ParamArg Pa,
+    const Template<float>* __restrict__ Tp, const StepArgs a, const hgk::RetrimArgs r, int32_t tb) {
+    if ((int32_t)blockIdx.x < tb) {
+        hgk::retrim_jobs(r, blockIdx.x, tb);
+        return;
+    }
+    step_body<TASK, false, true, true, false, BAKED, false>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a,
+                                                             (int64_t)blockIdx.x - tb);
+}
+#endif
 
 #ifdef HG_RTC   // step_rtc.hip: the step kernel's code and nothing else
 }  // namespace
@@ -1134,21 +1156,16 @@ struct hg_env {
     int32_t* retrim_ring = nullptr;         // [3] jobs of a step's re-trim: step k counts into [k % 3] and
     uint64_t retrim_gen = 0;                //     zeroes [(k + 1) % 3] from its kernel (no memset launch)
     uint64_t retrim_chain = kChainBroken;   // chain key of the previous re-trim step (see chain_key)
-    // ov mode (reset_mode RETRIM with next-step auto-reset): the episodes a step ends are re-trimmed on a
-    // side stream while the next step runs.  Step k queues its ends into ov_recs[k % 3] / ov_ring[k % 3];
-    // step k+1's call forks their trim (after step k) onto ov_side[k % 2], launches step k+1 -- which
-    // stores only the step counter of those envs -- and joins the trim back before returning, so the
-    // caller's stream sees step k+1 complete.  Consecutive trims overlap each other too (one side stream
-    // each), and every step waits only for the trim of the ends of the step before the previous one.
+    // ov mode (reset_mode RETRIM with next-step auto-reset): the episodes a step ends are re-trimmed
+    // while the next step runs.  Step k queues its ends into ov_recs[k % 3] / ov_ring[k % 3]; step k+1
+    // is one launch of step_ov_kernel holding their trims and the step, whose due resets store only
+    // their step counter (the trims write the rest, and their observation rows).
     bool ov = false;                        // configured (RETRIM + next-step auto-reset) and enabled
     bool ov_enabled = true;                 // hg_set_retrim_overlap
     uint64_t ov_chain = kChainBroken;       // chain key of the previous step when its ends can be trimmed
                                             // concurrently with this one (no other call in between)
     int4* ov_recs = nullptr;                // [3][N] jobs {env, trim wind}
     int32_t* ov_ring = nullptr;             // [3] their counts
-    hipStream_t ov_side[2] = {nullptr, nullptr};
-    hipEvent_t ov_fork[3] = {nullptr, nullptr, nullptr};   // after step k's launch: its trim may start
-    hipEvent_t ov_join[2] = {nullptr, nullptr};            // a side stream's trim is done
     float* tmpl_env = nullptr;              // per-env reset templates [N][39] (hg_set_reset_templates)
     bool env_templates = false;
     bool baked = false;                     // step with the constant-specialised kernel (baked.h)
@@ -1317,6 +1334,27 @@ static void dispatch_task(const hg_env* e, hipStream_t s, const StepArgs& a, boo
     }
 }
 
+// ov mode's launch: `ov_trim_blocks` trim blocks (the previous step's ends; blocks without a job exit at
+// once) ahead of the step's blocks
+static inline int32_t ov_trim_blocks(int64_t n) {
+    const int64_t b = n / 256;
+    return (int32_t)(b < 64 ? 64 : (b > 1024 ? 1024 : b));
+}
+static void launch_step_ov(const hg_env* e, hipStream_t s, const StepArgs& a, const hgk::RetrimArgs& r) {
+    const int32_t tb = ov_trim_blocks(e->n);
+    const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock) + (unsigned)tb;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kStepBlock), 0, s, STEP_KARGS(e), a, r, tb);
+    };
+    switch (e->cfg.task) {
+        case HG_TASK_HOVER: e->baked ? go(step_ov_kernel<HG_TASK_HOVER, true>) : go(step_ov_kernel<HG_TASK_HOVER, false>); break;
+        case HG_TASK_FORWARD_FLIGHT:
+            e->baked ? go(step_ov_kernel<HG_TASK_FORWARD_FLIGHT, true>) : go(step_ov_kernel<HG_TASK_FORWARD_FLIGHT, false>);
+            break;
+        default: e->baked ? go(step_ov_kernel<HG_TASK_HELI, true>) : go(step_ov_kernel<HG_TASK_HELI, false>); break;
+    }
+}
+
 extern "C" {
 #if HG_TIMING
 int hg_debug_timing(void* dst, int64_t bytes) {
@@ -1418,12 +1456,6 @@ static void release(hg_env* e) {
     dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_recs);
     dfree(e->retrim_count); dfree(e->retrim_ring); dfree(e->ov_recs); dfree(e->ov_ring);
     dfree(e->tmpl_env); dfree(e->setup_batch);
-    for (hipStream_t& q : e->ov_side)
-        if (q) (void)hipStreamDestroy(q);
-    for (hipEvent_t& v : e->ov_fork)
-        if (v) (void)hipEventDestroy(v);
-    for (hipEvent_t& v : e->ov_join)
-        if (v) (void)hipEventDestroy(v);
     delete e;
 }
 
@@ -1502,20 +1534,11 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
                            (float)e->Pd.wm[0], (float)e->Pd.wm[1], (float)e->Pd.wm[2]);
         if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "fill_wind_kernel");
 
-        if (cfg->autoreset && cfg->autoreset_mode == HG_AUTORESET_NEXT_STEP) {   // ov mode's buffers, streams, events
+        if (cfg->autoreset && cfg->autoreset_mode == HG_AUTORESET_NEXT_STEP) {   // ov mode's job rings
             if ((err = hipMalloc(&e->ov_recs, sizeof(int4) * 3 * num_envs)) != hipSuccess)
                 return cleanup(err, "hipMalloc ov jobs");
             if ((err = hipMalloc(&e->ov_ring, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc ov ring");
             if ((err = hipMemset(e->ov_ring, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset ov ring");
-            for (hipStream_t& q : e->ov_side)
-                if ((err = hipStreamCreateWithFlags(&q, hipStreamNonBlocking)) != hipSuccess)
-                    return cleanup(err, "hipStreamCreate ov");
-            for (hipEvent_t& v : e->ov_fork)
-                if ((err = hipEventCreateWithFlags(&v, hipEventDisableTiming)) != hipSuccess)
-                    return cleanup(err, "hipEventCreate ov");
-            for (hipEvent_t& v : e->ov_join)
-                if ((err = hipEventCreateWithFlags(&v, hipEventDisableTiming)) != hipSuccess)
-                    return cleanup(err, "hipEventCreate ov");
             e->ov = true;
         }
     }
@@ -1531,7 +1554,6 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
 void hg_destroy(hg_env* e) {
     if (!e) return;
     DevGuard dev_guard(e);
-    if (e->ov) (void)hipDeviceSynchronize();   // trims queued on the side streams
     release(e);
 }
 
@@ -1674,42 +1696,21 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     int32_t* rt_count = nullptr;
     int32_t rt_slot = -1;
     const bool ov = retrim && e->ov && e->ov_enabled;
-    // ov mode: the previous step's ends are trimmed concurrently with this step when it was this
-    // sequence's previous launch (no other call in between; not across captures or from an eager step
-    // after a capture, whose graphs may have run in between)
-    const bool ov_active = ov && e->ov_chain == key && !eager_after_capture;
-    int ov_side = -1;
+    // ov mode: the previous step's ends are trimmed in this step's launch (step_ov_kernel) when it was
+    // this sequence's previous launch (no other call in between; not across captures or from an eager
+    // step after a capture, whose graphs may have run in between), for the lone-wave sizes, in-kernel
+    // noise and the library's own kernels; otherwise this step's due resets take the serial re-trim
+    const bool ov_active = ov && e->ov_chain == key && !eager_after_capture && !eta && !e->rtc &&
+                           e->n <= HG_NT_WAVES * e->resident_envs;
     if (retrim) {   // the step's re-trim job count: a slot of the ring, zeroed by the previous step's kernel
         rt_slot = (int32_t)(e->retrim_gen % 3);
         rt_count = e->retrim_ring + rt_slot;
-        ov_side = (int)((e->retrim_gen + 1) & 1);   // = (k - 1) & 1 for the trim of step k - 1's ends
         ++e->retrim_gen;
         if (e->retrim_chain != key || eager_after_capture) {
             HIP_TRY(hipMemsetAsync(rt_count, 0, sizeof(int32_t), s));
             if (ov) HIP_TRY(hipMemsetAsync(e->ov_ring + rt_slot, 0, sizeof(int32_t), s));
         }
         e->retrim_chain = key;
-    }
-    if (ov_active) {   // the previous step's ends: trimmed on a side stream, concurrently with this step
-        const int prev = rt_slot == 0 ? 2 : rt_slot - 1;
-        hipStream_t side = e->ov_side[ov_side];
-        HIP_TRY(hipStreamWaitEvent(side, e->ov_fork[prev], 0));
-        hgk::RetrimArgs r;
-        memset(&r, 0, sizeof(r));
-        r.P = e->pd_dev;
-        r.T = e->setup_dev;
-        r.count = e->ov_ring + prev;
-        r.recs = e->ov_recs + (int64_t)prev * e->n;
-        r.state = e->state;
-        r.az = e->az;
-        r.obs = obs;
-        r.n = e->n;
-        r.fail_count = e->retrim_count + 1;
-        r.ov = 1;
-        r.tmpl = reinterpret_cast<const float*>(e->tmpl_dev);
-        r.tmpl_env = e->Pf.env_templates ? e->tmpl_env : nullptr;
-        HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), side));
-        HIP_TRY(hipEventRecord(e->ov_join[ov_side], side));
     }
     StepArgs a;
     a.hmap = e->hmap;
@@ -1737,13 +1738,28 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.ov_active = ov_active ? 1 : 0;
     const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next ||
                       e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
-    dispatch_task<false>(e, s, a, eta != nullptr, feat);
-    HIP_TRY(hipGetLastError());
-    if (ov) {
-        HIP_TRY(hipEventRecord(e->ov_fork[rt_slot], s));   // this step's ends may be trimmed from here on
-        if (ov_active) HIP_TRY(hipStreamWaitEvent(s, e->ov_join[ov_side], 0));
-        e->ov_chain = key;
+    if (ov_active) {   // the previous step's ends trimmed in this launch's first blocks
+        const int prev = rt_slot == 0 ? 2 : rt_slot - 1;
+        hgk::RetrimArgs r;
+        memset(&r, 0, sizeof(r));
+        r.P = e->pd_dev;
+        r.T = e->setup_dev;
+        r.count = e->ov_ring + prev;
+        r.recs = e->ov_recs + (int64_t)prev * e->n;
+        r.state = e->state;
+        r.az = e->az;
+        r.obs = obs;
+        r.n = e->n;
+        r.fail_count = e->retrim_count + 1;
+        r.ov = 1;
+        r.tmpl = reinterpret_cast<const float*>(e->tmpl_dev);
+        r.tmpl_env = e->Pf.env_templates ? e->tmpl_env : nullptr;
+        launch_step_ov(e, s, a, r);
+    } else {
+        dispatch_task<false>(e, s, a, eta != nullptr, feat);
     }
+    HIP_TRY(hipGetLastError());
+    if (ov) e->ov_chain = key;
     if (retrim && !ov_active) {   // re-trim this step's resets against their last wind (overwrites the template)
         hgk::RetrimArgs r;
         memset(&r, 0, sizeof(r));

@@ -1,0 +1,431 @@
+// retrim_body.h -- the device batched Newton trim's per-job body (HelicopterDynamics.trim,
+// helicopter_dynamics.py:491-555), shared by retrim.hip's retrim_kernel and the overlapped next-step
+// re-trim kernel of heligym_amd.hip.  Both translation units build it with -ffp-contract=on (fused
+// multiply-adds per source expression, decided by the front end), so the two kernels round every
+// trim identically.
+#pragma once
+
+#include "retrim.h"
+
+namespace hgk {
+namespace {
+
+#ifndef HG_TIMING
+#define HG_TIMING 0
+#endif
+#if HG_TIMING
+// diagnostic build: s_memtime at the phase boundaries of the first job's rounds (lane 0)
+__device__ unsigned long long g_rt_timing[64];
+#define RSTAMP(j, ...)                                                                \
+    do {                                                                              \
+        asm volatile("" ::__VA_ARGS__);                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                   \
+        if (l == 0 && job == 0 && (j) < 64) g_rt_timing[(j)] = t_;                    \
+    } while (0)
+#else
+#define RSTAMP(j, ...) do { } while (0)
+#endif
+
+__device__ __forceinline__ double read_lane(double v, int lane) {
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)u, lane);
+    const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// The wave is the block: its LDS operations execute in issue order, so a read issued after a write
+// sees it.  This only keeps the compiler from reordering LDS accesses across the point.
+__device__ __forceinline__ void lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// 1 / x for a finite non-zero x: v_rcp_f64 and two Newton steps (fused), within an ulp
+__device__ __forceinline__ double rcp_f64(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return fma(r, fma(-x, r, 1.0), r);
+}
+
+// max of a 32-bit key over each row of 16 lanes (DPP row rotations; every lane has a source)
+__device__ __forceinline__ uint32_t row16_max(uint32_t k) {
+    k = max(k, (uint32_t)__builtin_amdgcn_mov_dpp((int)k, 0x128, 0xF, 0xF, true));
+    k = max(k, (uint32_t)__builtin_amdgcn_mov_dpp((int)k, 0x124, 0xF, 0xF, true));
+    k = max(k, (uint32_t)__builtin_amdgcn_mov_dpp((int)k, 0x122, 0xF, 0xF, true));
+    k = max(k, (uint32_t)__builtin_amdgcn_mov_dpp((int)k, 0x121, 0xF, 0xF, true));
+    return k;
+}
+
+// np.linalg.inv(dydx) @ r (helicopter_dynamics.py:524-527) as Gauss-Jordan with partial pivoting,
+// one row per lane: lane l holds row i = l & 15 of [J | r] (the four rows of 16 lanes are identical
+// copies).  Per pivot step C (unrolled, so every column index is a register):
+//   * the pivot is the unused row with the largest |J[i][C]|, found with a DPP max over the 16 rows
+//     on the high word of |J[i][C]| (monotonic in |x|; rows within 2^-20 of the maximum tie and the
+//     lowest row wins: any of them is as good a pivot, partial pivoting only needs a large one);
+//   * the pivot row is read with readlanes (its row index is uniform), each row subtracts
+//     (J[i][C] / pivot) x the pivot row with one fused multiply-add per element, and the pivot row
+//     is scaled by 1 / pivot;
+//   * rows never move: each remembers the column it was the pivot of, and the solution is the
+//     right-hand side in that order.
+// Columns < C are neither read nor updated after step C (the host's solve16 updates them and never
+// reads them again).  Fused arithmetic and a different tie rule make this a different rounding of
+// the same solve (the trims are compared with the host's to fp32 resolution, not bitwise).
+// A zero or non-finite pivot (a singular or non-finite system) makes its reciprocal, and with it the
+// solution, non-finite: the caller checks the solution once instead of every pivot.
+#ifndef HG_GJ_NOSCALE   // 1: the pivot rows stay unscaled, each row's solution divided at the end
+#define HG_GJ_NOSCALE 0
+#endif
+#ifndef HG_GJ_LDS       // 1: the pivot row reaches the other rows through LDS (broadcast reads)
+#define HG_GJ_LDS 0
+#endif
+constexpr int kRowStride = 18;   // doubles per LDS row (16-byte aligned pairs)
+
+template <int C>
+__device__ __forceinline__ void gj_step(double (&A)[16], double& b, uint32_t& live, int& mycol, int i,
+                                        double& myinv, double* sRow, int l) {
+    (void)myinv; (void)sRow; (void)l;
+    const double v = A[C];
+    // |v|'s high word with the top bit set (so that a zero candidate still beats a used row); 0 once used
+    const uint32_t key = ((uint32_t)(__double_as_longlong(v) >> 32) | 0x80000000u) & live;
+    const double own_inv = rcp_f64(v);   // every row's reciprocal while the search runs (off its chain)
+    const uint32_t mx = row16_max(key);
+    const uint32_t hit = (uint32_t)__ballot(key == mx) & 0xFFFFu;   // rows of the first 16 lanes
+    const int P = __builtin_ctz(hit | 0x10000u);
+    const double rinv = read_lane(own_inv, P);
+    const bool piv = i == P;
+#if HG_GJ_LDS
+    // every row's live part to its LDS row, then the pivot row read back by all (broadcast)
+    constexpr int k0 = (C + 1) >> 1;
+    double* mine = sRow + l * kRowStride;
+#pragma unroll
+    for (int k = k0; k < 8; ++k) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        *reinterpret_cast<d2*>(mine + 2 * k) = d2{A[2 * k], A[2 * k + 1]};
+    }
+    mine[16] = b;
+    lds_order();
+    double pr[17];
+    const double* prow = sRow + P * kRowStride;
+#pragma unroll
+    for (int k = k0; k < 8; ++k) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        const d2 t = *reinterpret_cast<const d2*>(prow + 2 * k);
+        pr[2 * k] = t.x;
+        pr[2 * k + 1] = t.y;
+    }
+    pr[16] = prow[16];
+#define HG_PJ(j) pr[j]
+#define HG_PB pr[16]
+#else
+#define HG_PJ(j) read_lane(A[j], P)
+#define HG_PB read_lane(b, P)
+#endif
+#if HG_GJ_NOSCALE
+    // rows are never scaled: other rows subtract (v / pivot) x the pivot row, the pivot row keeps its
+    // values (the fused add of -0 is exact) and its reciprocal divides its right-hand side at the end
+    const double g = piv ? 0.0 : v * rinv;
+#pragma unroll
+    for (int j = C + 1; j < 16; ++j) A[j] = fma(-g, HG_PJ(j), A[j]);
+    b = fma(-g, HG_PB, b);
+    myinv = piv ? rinv : myinv;
+#else
+    // other rows: A - (v / pivot) pj; the pivot row: A / pivot -- one form for both, A * m - g pj with
+    // (m, g) = (1, v / pivot) or (1 / pivot, 0): the product by 1 and the fused add of -0 are exact
+    const double g = piv ? 0.0 : v * rinv;
+    const double m = piv ? rinv : 1.0;
+#pragma unroll
+    for (int j = C + 1; j < 16; ++j) A[j] = fma(-g, HG_PJ(j), A[j] * m);
+    b = fma(-g, HG_PB, b * m);
+#endif
+#undef HG_PJ
+#undef HG_PB
+    live = piv ? 0u : live;
+    mycol = piv ? C : mycol;
+}
+template <int C>
+__device__ __forceinline__ void gj_steps(double (&A)[16], double& b, uint32_t& live, int& mycol, int i,
+                                         double& myinv, double* sRow, int l) {
+    gj_step<C>(A, b, live, mycol, i, myinv, sRow, l);
+    if constexpr (C < 15) gj_steps<C + 1>(A, b, live, mycol, i, myinv, sRow, l);
+}
+
+// What the observation needs from one evaluation beyond the state: power, uvw_air, ned velocity
+// (observe(), helicopter_dynamics.py:471-488).
+struct EvalExt {
+    double o[7];
+};
+
+// __trim_fcn (helicopter_dynamics.py:557-576, trim.h trim_fcn): the normalised derivatives y(x) at
+// one trial point, and the observation's non-state terms.
+__device__ __forceinline__ void trim_eval(const hg::Params<double>& P, const hg::TrimSetup& T, const double x[16],
+                                          const double W[3], double y[16], EvalExt& e) {
+    double s[18], d[18];
+    hg::trim_state(P, T.base, x, s);
+    const hg::Controls<double> u = hg::controls(P, x[12], x[13], x[14], x[15]);
+    hg::Attitude<double> att;
+    hg::m_sincos(s[12], &att.s[0], &att.c[0]);
+    hg::m_sincos(s[13], &att.s[1], &att.c[1]);
+    att.s[2] = T.s_psi;
+    att.c[2] = T.c_psi;
+    const hg::Frame<double> f = hg::frame(P, s, W, T.hc, att, T.rho_irho);
+    const hg::Loads<double> A = hg::main_loads(P, s, u, f);
+    const hg::Loads<double> B = hg::tail_loads(P, s, u, f);
+    hg::eom(P, s, f, A, B, d);
+    y[0] = hg::m_div_c(d[0], P.mr_VTIP, P.mr_inv_VTIP);
+    y[1] = hg::m_div_c(d[1], P.tr_VTIP, P.tr_inv_VTIP);
+    y[2] = d[4];
+    y[3] = d[5];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        y[4 + k] = hg::m_div_c(d[6 + k], P.mr_VTIP, P.mr_inv_VTIP);
+        y[7 + k] = hg::m_div_c(d[9 + k], P.mr_OMEGA, P.mr_inv_OMEGA);
+        y[10 + k] = d[12 + k];
+        y[13 + k] = hg::m_div_c(d[15 + k], P.mr_R, P.mr_inv_R);
+    }
+    e.o[0] = ((A.power + B.power) + P.p_loss) * (1.0 / 550.0);
+    e.o[1] = f.ua; e.o[2] = f.va; e.o[3] = f.wa;
+    e.o[4] = f.n0; e.o[5] = f.n1; e.o[6] = f.n2;
+}
+
+__device__ __forceinline__ void retrim_write(const RetrimArgs& a, const hg::Params<double>& P, const hg::TrimSetup& T,
+                                             int64_t job, int64_t env, const double x[16], const double* ext) {
+    double s[18], ob[17];
+    hg::trim_state(P, T.base, x, s);
+#pragma unroll
+    for (int c = 0; c < 7; ++c) ob[c] = ext[c];
+    ob[7] = s[12]; ob[8] = s[13]; ob[9] = s[14];
+    ob[10] = s[9]; ob[11] = s[10]; ob[12] = s[11];
+    ob[13] = s[15]; ob[14] = s[16]; ob[15] = -s[17]; ob[16] = -T.hc.zh(s[17]);
+    if (a.list || a.recs) {
+        for (int c = 0; c < 18; ++c)
+            if (has_slot(c)) a.state[tix(env, c)] = (float)s[c];
+        int32_t* ctr = reinterpret_cast<int32_t*>(a.state);
+        int32_t epi = ctr[tix(env, kCtrCol0 + 2)];
+        if (a.ov) {   // the rest of the reset (the concurrent step stored the step counter)
+            epi += 1;
+            for (int c = 18; c < 23; ++c) a.state[tix(env, c)] = 0.f;
+            ctr[tix(env, kCtrCol0 + 1)] = 0;
+            ctr[tix(env, kCtrCol0 + 2)] = epi;
+        }
+        a.az[env] = AzRec{(float)s[kAzCol0], (float)s[kAzCol0 + 1], 0, epi};   // the reset's step 0
+        const int co[4] = {4, 5, 6, 16};
+        for (int c = 0; c < 4; ++c) a.state[tix(env, 23 + c)] = (float)ob[co[c]];
+        if (a.obs)
+            for (int c = 0; c < 17; ++c) a.obs[env * 17 + c] = (float)ob[c];
+    } else {
+        if (a.out_state)
+            for (int c = 0; c < 18; ++c) a.out_state[job * 18 + c] = (float)s[c];
+        if (a.out_action)
+            for (int c = 0; c < 4; ++c) a.out_action[job * 4 + c] = (float)x[12 + c];
+        if (a.out_obs)
+            for (int c = 0; c < 17; ++c) a.out_obs[job * 17 + c] = (float)ob[c];
+    }
+    if (a.out_status) a.out_status[job] = HG_OK;
+}
+
+// ov mode, a failed trim: the env takes the template reset the step would have stored (the
+// reference raises instead, helicopter_dynamics.py:543-544; the failure is counted)
+__device__ __forceinline__ void retrim_write_template(const RetrimArgs& a, int64_t env) {
+    const float* tr = a.tmpl_env ? a.tmpl_env + env * 39 : a.tmpl;
+    for (int c = 0; c < 18; ++c)
+        if (has_slot(c)) a.state[tix(env, c)] = tr[c];
+    for (int c = 18; c < 23; ++c) a.state[tix(env, c)] = 0.f;
+    for (int c = 0; c < 4; ++c) a.state[tix(env, 23 + c)] = tr[18 + c];
+    int32_t* ctr = reinterpret_cast<int32_t*>(a.state);
+    const int32_t epi = ctr[tix(env, kCtrCol0 + 2)] + 1;
+    ctr[tix(env, kCtrCol0 + 1)] = 0;
+    ctr[tix(env, kCtrCol0 + 2)] = epi;
+    // an episode begun from the template: the azimuth record anchors the template's azimuths
+    a.az[env] = AzRec{tr[kAzCol0], tr[kAzCol0 + 1], 0, epi};
+    if (a.obs)
+        for (int c = 0; c < 17; ++c) a.obs[env * 17 + c] = tr[22 + c];
+}
+
+// One wave per trim.  Each evaluation round evaluates 42 points at once: lanes 0..31 the +-eps
+// Jacobian columns around the point the next Newton step starts from, lanes 32..41 the ten
+// step-halving trials of the current step (trial 0, the full step, is that point whenever the
+// search accepts it, which it usually does; the first round: lane 32 the residual at x0).  The first
+// trial that lowers the residual is the one the reference's sequential search accepts
+// (helicopter_dynamics.py:530-541).  When the search accepts a shorter step, a round of Jacobian
+// lanes alone re-evaluates around it (the trial lanes keep their values).  Then the evaluations go
+// through LDS to the Gauss-Jordan solve.  A trim of three Newton steps takes four rounds and three
+// solves.
+enum : int { kRoundFirst = 0, kRoundNormal = 1, kRoundJacobian = 2 };
+
+// Model constants and trim setup through the constant address space: scalar loads (the kernel's
+// stores cannot alias them), re-issued each round (opaque pointers) instead of hoisted out of the
+// Newton loop, where ~180 fp64 values would stay live in registers.
+typedef __attribute__((address_space(4))) const hg::Params<double> ConstP;
+typedef __attribute__((address_space(4))) const hg::TrimSetup ConstT;
+template <typename Q, typename T>
+__device__ __forceinline__ const T& opaque_const(const T* p) {
+    Q* c = (Q*)p;
+    asm volatile("" : "+s"(c));
+    return *(const T*)c;
+}
+
+#ifndef HG_RETRIM_WAVES
+#define HG_RETRIM_WAVES 2
+#endif
+// The jobs first, first + stride, ... of a batch, one wave (this block) per trim: retrim_kernel and the
+// trim blocks of the overlapped next-step re-trim (heligym_amd.hip step_ov_kernel).
+__device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, int64_t stride) {
+    __shared__ double sE[32 * 16];   // the +-eps evaluations E[j][k] of the current Newton step
+    __shared__ double sR[16];        // its right-hand side y - y*
+    __shared__ double sX[16];        // the solution (Newton direction), by column
+    __shared__ double sExt[7];       // observation terms of the current iterate
+    __shared__ double sRow[HG_GJ_LDS ? 64 * kRowStride : 2];   // HG_GJ_LDS: the rows of the solve
+    const int l = threadIdx.x;
+    const hg::Params<double>& P = *a.P;
+    const double eps = hg::kTrimEps;
+    const int c = l & 15;            // Jacobian column of lanes 0..31
+    const int j = l - 32;            // line-search trial of lanes 32..41
+    // the first job record is requested with the job count (the grid never exceeds the list: blocks
+    // <= min(n, 1024)), so the start waits for one load, not two dependent ones
+    const int4 rec0 = a.recs ? a.recs[first] : make_int4(0, 0, 0, 0);
+    int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
+    if (a.count && jobs > a.n) jobs = a.n;   // a queue holds at most one job per env
+    for (int64_t job = first; job < jobs; job += stride) {   // uniform per wave
+        const int4 rec = a.recs ? (job == first ? rec0 : a.recs[job]) : make_int4(0, 0, 0, 0);
+        const int64_t env = a.recs ? (int64_t)rec.x : (a.list ? (int64_t)a.list[job] : job);
+        const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];
+        double W[3] = {P.wm[0], P.wm[1], P.wm[2]};   // NULL wind: the mean wind (helicopter.py:55)
+        if (a.recs) {
+            W[0] = (double)__int_as_float(rec.y);
+            W[1] = (double)__int_as_float(rec.z);
+            W[2] = (double)__int_as_float(rec.w);
+        } else if (a.wind && a.wind_soa) {
+            W[0] = (double)a.wind[env];
+            W[1] = (double)a.wind[a.n + env];
+            W[2] = (double)a.wind[2 * a.n + env];
+        } else if (a.wind) {
+            const float* wr = a.wind + 3 * (a.list ? env : job);
+            W[0] = (double)wr[0];
+            W[1] = (double)wr[1];
+            W[2] = (double)wr[2];
+        }
+        double x[16], dir[16], ye[16], te = 0.0;
+        EvalExt ext;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; ye[k] = 0.0; }
+        double tol = 0;
+        int it = 0, kind = kRoundFirst, src = 32, round = 0;
+        bool ok = true, converged = false;
+        RSTAMP(0, "v"(l));
+        while (true) {
+            const hg::Params<double>& P = opaque_const<ConstP>(a.P);
+            const hg::TrimSetup& T = opaque_const<ConstT>(a.T + (a.setup_stride ? job : 0));
+            // ---- one evaluation round (every x - s dir is the same fused operation wherever formed)
+            double xe[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const double base = kind == kRoundNormal ? fma(-1.0, dir[k], x[k]) : x[k];
+                double v;
+                if (l < 32) {
+                    v = k == c ? (l < 16 ? base + eps : base - eps) : base;
+                } else {
+                    const double step = (kind == kRoundNormal && j < hg::kTrimLineSearch) ? ldexp(1.0, -j) : 0.0;
+                    v = fma(-step, dir[k], x[k]);
+                }
+                xe[k] = v;
+            }
+            RSTAMP(1 + 4 * round, "v"(xe[0]));
+            if (kind != kRoundJacobian || l < 32) {
+                trim_eval(P, T, xe, W, ye, ext);
+                double t = 0.0;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) t = fma(ye[k] - T.yt[k], ye[k] - T.yt[k], t);
+                te = t;
+            }
+            RSTAMP(2 + 4 * round, "v"(te));
+            if (kind != kRoundJacobian) {
+                // ---- accept a trial (or take the base point)
+                bool have_jac = true;
+                if (kind == kRoundNormal) {
+                    const unsigned long long lower = __ballot(j >= 0 && j < hg::kTrimLineSearch && te < tol) >> 32;
+                    const int js = lower ? __builtin_ctzll(lower) : hg::kTrimLineSearch;
+                    if (js >= hg::kTrimLineSearch - 1) break;   // helicopter_dynamics.py:540: keep x
+                    const double step = ldexp(1.0, -js);
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) x[k] = fma(-step, dir[k], x[k]);
+                    src = 32 + js;
+                    have_jac = js == 0;   // the Jacobian lanes evaluated around trial 0
+                    if (++it > hg::kTrimMaxIter) { ok = false; break; }
+                }
+                tol = read_lane(te, src);
+                if (!(tol > eps)) { converged = true; break; }   // the accepting lane holds the final evaluation
+                if (l == src) {
+#pragma unroll
+                    for (int k = 0; k < 7; ++k) sExt[k] = ext.o[k];
+                }
+                if (!have_jac) {   // the search accepted a shorter step: Jacobian at the new x first
+                    kind = kRoundJacobian;
+                    ++round;
+                    continue;
+                }
+            }
+            // ---- Newton direction: the evaluations and the residual (lane src holds y) into LDS,
+            // then the solve, one row per lane
+            lds_order();   // the previous solve's reads are done
+            if (l < 32) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) sE[l * 16 + k] = ye[k];
+            }
+            if (l == src) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) sR[k] = ye[k] - T.yt[k];
+            }
+            lds_order();
+            RSTAMP(3 + 4 * round, "v"(ye[0]));
+            {
+                const int i = l & 15;
+                double A[16], Em[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {   // all 33 reads issued before the first use
+                    A[q] = sE[q * 16 + i];
+                    Em[q] = sE[(q + 16) * 16 + i];
+                }
+                double b = sR[i];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) A[q] = (A[q] - Em[q]) * (0.5 / eps);
+                uint32_t live = 0xFFFFFFFFu;   // the key mask of a row not yet used as a pivot
+                int mycol = 0;
+                double myinv = 1.0;
+                gj_steps<0>(A, b, live, mycol, i, myinv, sRow, l);
+                if (l < 16) sX[mycol] = HG_GJ_NOSCALE ? b * myinv : b;
+                lds_order();
+                bool fin = true;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    dir[k] = sX[k];
+                    fin = fin && isfinite(dir[k]);
+                }
+                if (!fin) { ok = false; break; }
+            }
+            RSTAMP(4 + 4 * round, "v"(dir[0]));
+            kind = kRoundNormal;
+            ++round;
+        }
+        RSTAMP(63, "v"(l));
+        if (ok) {
+            if (converged) {
+                if (l == src) retrim_write(a, P, T, job, env, x, ext.o);
+            } else if (l == 0) {
+                // the search stopped without converging (:540): the kept x and its evaluation
+                double e[7];
+                lds_order();
+#pragma unroll
+                for (int k = 0; k < 7; ++k) e[k] = sExt[k];
+                retrim_write(a, P, T, job, env, x, e);
+            }
+        } else if (l == 0) {
+            if (a.ov) retrim_write_template(a, env);
+            if (a.fail_count) atomicAdd(a.fail_count, 1);
+            if (a.out_status) a.out_status[job] = HG_E_TRIM;
+        }
+        lds_order();   // the next job's writes come after this job's reads
+    }
+}
+
+}  // namespace
+}  // namespace hgk

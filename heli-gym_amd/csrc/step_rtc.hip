@@ -20,7 +20,7 @@
     extern "C" __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) void name( \
         float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p, ParamArg Pa,        \
         const Template<float>* __restrict__ Tp, const StepArgs a) {                                      \
-        step_body<HG_RTC_TASK, false, NT, FEAT, false, true, NTS>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a); \
+        step_body<HG_RTC_TASK, false, NT, FEAT, false, true, NTS>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a, blockIdx.x); \
     }
 
 // names and order: hg_load_specialized (heligym_amd.hip) looks them up by these names

@@ -296,12 +296,13 @@ int32_t hg_retrim_failures(hg_env* env, int64_t* count);
 
 /* HG_RESET_RETRIM with next-step auto-reset (gymnasium's default, make_vec's): the episodes a step ends
  * are re-trimmed (helicopter.py:208-212 -> helicopter_dynamics.py:491-555) while the next step runs,
- * on internal side streams forked from and joined back into the caller's stream within each step
- * call, so the stream still sees every step complete, results bitwise the serial path's.  A step
- * overlaps the trim of the previous step's ends only when that step was the previous launch of the
- * same sequence (eager, or captured into the same graph) with no other call on the handle in between;
- * otherwise its due resets are trimmed after it, serially.  enable = 1 (the default) or 0 (always
- * serial: A/B and tests).  Returns 1 if the mode is configured and enabled, 0 otherwise, or HG_E_*. */
+ * in the same kernel launch as that step (its first blocks), so the caller's stream sees every step
+ * complete and the results are bitwise the serial path's.  A step holds the trims of the previous
+ * step's ends only when that step was the previous launch of the same sequence (eager, or captured
+ * into the same graph) with no other state-changing call on the handle in between, with in-kernel
+ * noise and at most two step waves per SIMD (N <= 131 072 on MI355X); otherwise its due resets are
+ * trimmed after it, serially.  enable = 1 (the default) or 0 (always serial: A/B and tests).
+ * Returns 1 if the mode is configured and enabled, 0 otherwise, or HG_E_*. */
 int32_t hg_set_retrim_overlap(hg_env* env, int32_t enable);
 
 /* State access for parity tests / checkpointing (the reference's StateNumpy,

@@ -12,3 +12,5 @@ timeout -k 10 200 python scripts/retrim_modes.py > gpurun_out/r04_retrim_modes.t
 grep -v amdgpu.ids gpurun_out/r04_retrim_modes.txt
 timeout -k 10 200 python scripts/r04_window_probe.py > gpurun_out/r04_window_probe.txt 2>&1 || { echo "window probe failed"; tail -5 gpurun_out/r04_window_probe.txt; exit 5; }
 grep -v amdgpu.ids gpurun_out/r04_window_probe.txt
+OV=1 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ovtrace1 -o run -- python3 scripts/r04_ov_trace.py > gpurun_out/ovtrace1.txt 2>&1 || { echo "ov trace failed"; exit 6; }
+grep -h "us/step" gpurun_out/ovtrace1.txt

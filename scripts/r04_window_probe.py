@@ -31,15 +31,11 @@ torch.cuda.synchronize()
 s = torch.cuda.Stream(device=dev)
 
 
-def capture(steps, events=None):
+def capture(steps):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-        if events:
-            events[0].record()
         for k in range(steps):
             env.step_async(bank[k % B], with_reset_info=False)
-        if events:
-            events[1].record()
     return g
 
 
@@ -91,19 +87,6 @@ rep("graph(K), no preroll", lambda: window(gK.replay, None, False))
 rep("eager(K), preroll graph(100)", lambda: window(eager, g100.replay, False))
 rep("graph(K) x2 back to back, per K", lambda: window(lambda: (gK.replay(), gK.replay()), g100.replay, False) / 2)
 rep("graph(100), preroll graph(100) [per 100/K]", lambda: window(g100.replay, g100.replay, False) * K / 100)
-ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
-gE = capture(K, ev)
-
-
-def inside():
-    torch.cuda.synchronize()
-    g100.replay()
-    gE.replay()
-    torch.cuda.synchronize()
-    return ev[0].elapsed_time(ev[1]) * 1e3 / K
-
-
-rep("events captured inside graph(K)", inside)
 t0 = time.perf_counter()
 for _ in range(50):
     gK.replay()

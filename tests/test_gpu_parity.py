@@ -911,7 +911,7 @@ def test_retrim_overlap_bitwise_equals_serial(torch, graph_steps):
     serial, f0 = _retrim_next_step_run(torch, N, K, False, graph_steps)
     over, f1 = _retrim_next_step_run(torch, N, K, True, graph_steps)
     ends = int((serial[2] | serial[3]).sum())
-    assert ends > 300, ends   # re-trimmed resets happened, and many of them overlapped
+    assert ends > 200, ends   # re-trimmed resets happened, and many of them overlapped
     assert f0 == f1
     for j, (x, y) in enumerate(zip(serial, over)):
         np.testing.assert_array_equal(x, y, err_msg=f"output {j}")
