@@ -322,6 +322,12 @@ class Timer:
         return r + (n / repeats,)
 
 
+def progress(msg):
+    """One line per bench phase on stderr (the JSON line stays the last line of stdout): a run that
+    fails names the phase it failed in."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def graphs_for(torch, dev, one_step, K, B):
     """Exactly K steps: K // B replays of a hipGraph of B steps, then the K mod B remaining steps
     launched eagerly.  A graph launch costs the GPU about 8 us more than the same steps launched
@@ -658,6 +664,7 @@ def main():
         total_envs = CONFIG5_TOTAL
     else:
         N = args.envs
+        progress(f"headline: {N} envs")
         env = make_env(args, torch, N, rank * N, dev)
         bank = action_bank(args, torch, env, N, dev, B)
         aged = age(args, torch, env, bank, B)
@@ -684,6 +691,8 @@ def main():
             # the same step with the compacted reset info (same-step auto-reset: reset indices and
             # terminal observations compacted in-kernel; captured, so a memset node zeroes the count)
             if args.reset_mode == "template" and args.autoreset_mode == "same_step":
+                progress("step_with_reset_info / step_api_eager")
+
                 def one_step_ri(k):
                     env.step_async(bank[k % B], with_reset_info=True)
                 rep_ri, _k2 = graphs_for(torch, dev, one_step_ri, K, B)
@@ -711,6 +720,7 @@ def main():
                                          "(fields not read here; the reset info costs one nonzero when read)"}
             if env.specialized and not args.generic_kernel:
                 # the generic kernel (model constants loaded, any airframe); bitwise-identical results
+                progress("generic_kernel")
                 env.set_specialized(False)
                 rep_g, _k3 = graphs_for(torch, dev, one_step, K, B)
                 s_g, _, _, rs_g = timer.run_counted(env, rep_g, R)
@@ -720,12 +730,14 @@ def main():
                                                "value": total_envs * K / s_g, "unit": "env-steps/s",
                                                "ms_per_step": s_g / K * 1e3, "resets_in_window": rs_g}
             if world == 1 and args.task != "heli" and args.reset_mode == "template" and N <= 262144:
+                progress("airframes")
                 try:
                     secondary["airframes"] = airframes(args, torch, timer, N, dev, B, K, R, sec / K)
                 except Exception as exc:   # (hipcc missing, ...): report, never lose the line
                     secondary["airframes"] = {"error": repr(exc)}
             if args.rollout_steps > 0 and args.reset_mode == "template":
                 Rs = args.rollout_steps
+                progress("rollout")
                 rbank = bank if Rs == B else torch.stack([bank[k % B] for k in range(Rs)])
                 rout = env.rollout(rbank)
                 nroll = max(1, K // Rs)
@@ -749,6 +761,7 @@ def main():
             for name, mode in (("retrim", args.autoreset_mode), ("retrim_next_step", "next_step")):
                 if name == "retrim_next_step" and args.autoreset_mode == "next_step":
                     continue
+                progress(f"{name} ({mode})")
                 envr = make_env(argparse.Namespace(**{**vars(args), "reset_mode": "retrim", "autoreset_mode": mode}),
                                 torch, N, rank * N, dev)
 
@@ -767,6 +780,7 @@ def main():
                     "ms_per_step": s_rt / Kr * 1e3 if rs_rt > 0 else None, "window_ms_per_step": s_rt / Kr * 1e3,
                     "resets_in_window": rs_rt, "aged_steps": aged_r, "autoreset_mode": mode,
                     "steps": Kr, "retrim_failures": envr.retrim_failures(),
+                    "retrim_invalid_jobs": envr.retrim_invalid_jobs(),
                     "note": "reset_mode='retrim': each auto-reset re-trimmed on the device (Newton trim against the "
                             "env's last wind, the reference's reset from episode 2 on), hipGraph"
                             + ("; next-step auto-reset (make_vec's configuration): the episodes a step ends are "
@@ -777,6 +791,7 @@ def main():
             # the same step past the 256 MB Infinity Cache (1.32 GB moved per launch): HBM bytes, not
             # fabric bytes, with its own committed PMC summary
             Nx = OUT_OF_CACHE_ENVS
+            progress(f"out_of_cache: {Nx} envs")
             envx = make_env(args, torch, Nx, 0, dev)
             bankx = action_bank(args, torch, envx, Nx, dev, B)
             Kx = min(K, 200)

@@ -705,6 +705,18 @@ __global__ __launch_bounds__(kBlock) void mask_list_kernel(const uint8_t* mask, 
     if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
 }
 
+// Job counters zeroed ahead of the launch that counts into them.  A one-thread kernel, not
+// hipMemsetAsync: captured into a hipGraph, a 4-byte memset node left the counter non-zero on later
+// replays on MI355X (0x08080808 and stale counts in scripts/r04_retrim_fault.py), so the re-trim
+// read a job count past the records its step wrote; a kernel node keeps its arguments by value.
+__global__ __launch_bounds__(64) void zero_counts_kernel(int32_t* a, int32_t* b, int32_t* c) {
+    if (threadIdx.x == 0) {
+        if (a) *a = 0;
+        if (b) *b = 0;
+        if (c) *c = 0;
+    }
+}
+
 // The rotor azimuths (psi_mr, psi_tr): their rates are the constants Omega (helicopter_dynamics.py:
 // 257-258, :288-289), so RK4 adds dt/6 (O + 2 O + 2 O + O) = dt Omega (f_dpsi) per step, and
 // step_after wraps them to [-pi, pi) (:74-75).  The step kernel does not carry them; these are the
@@ -1152,7 +1164,7 @@ struct hg_env {
     float* retrim_wind = nullptr;           // reset_mode RETRIM work buffers
     int32_t* retrim_list = nullptr;         // hg_reset's masked envs (their winds by env)
     int4* retrim_recs = nullptr;            // a step's auto-reset jobs {env, wind}
-    int32_t* retrim_count = nullptr;        // [0] jobs of hg_reset's re-trim, [1] failures so far
+    int32_t* retrim_count = nullptr;        // [0] jobs of hg_reset's re-trim, [1] failures so far, [2] invalid jobs
     int32_t* retrim_ring = nullptr;         // [3] jobs of a step's re-trim: step k counts into [k % 3] and
     uint64_t retrim_gen = 0;                //     zeroes [(k + 1) % 3] from its kernel (no memset launch)
     uint64_t retrim_chain = kChainBroken;   // chain key of the previous re-trim step (see chain_key)
@@ -1258,6 +1270,12 @@ static int32_t build_template(hg_env* e) {
         if (err != hipSuccess) return fail(HG_E_HIP, std::string("template upload: ") + hipGetErrorString(err));
     }
     return HG_OK;
+}
+
+static hipError_t zero_counts(int32_t* const p[3], hipStream_t s) {
+    if (!p[0] && !p[1] && !p[2]) return hipSuccess;
+    hipLaunchKernelGGL(zero_counts_kernel, dim3(1), dim3(64), 0, s, p[0], p[1], p[2]);
+    return hipGetLastError();
 }
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -1519,8 +1537,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if ((err = hipMalloc(&e->pd_dev, sizeof(Params<double>))) != hipSuccess) return cleanup(err, "hipMalloc params64");
     if ((err = hipMemcpy(e->pd_dev, &e->Pd, sizeof(e->Pd), hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy params64");
-    if ((err = hipMalloc(&e->retrim_count, 2 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim");
-    if ((err = hipMemset(e->retrim_count, 0, 2 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim");
+    if ((err = hipMalloc(&e->retrim_count, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim");
+    if ((err = hipMemset(e->retrim_count, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim");
     if ((err = hipMalloc(&e->retrim_ring, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim ring");
     if ((err = hipMemset(e->retrim_ring, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim ring");
     if (cfg->reset_mode == HG_RESET_RETRIM) {
@@ -1530,6 +1548,9 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
             return cleanup(err, "hipMalloc retrim list");
         if ((err = hipMalloc(&e->retrim_recs, sizeof(int4) * num_envs)) != hipSuccess)
             return cleanup(err, "hipMalloc retrim jobs");
+        // job records never written name env -1: a trim reading one skips it (and counts it)
+        if ((err = hipMemset(e->retrim_recs, 0xFF, sizeof(int4) * num_envs)) != hipSuccess)
+            return cleanup(err, "hipMemset retrim jobs");
         hipLaunchKernelGGL(fill_wind_kernel, dim3(grid_for(num_envs)), dim3(kBlock), 0, 0, e->retrim_wind, num_envs,
                            (float)e->Pd.wm[0], (float)e->Pd.wm[1], (float)e->Pd.wm[2]);
         if ((err = hipGetLastError()) != hipSuccess) return cleanup(err, "fill_wind_kernel");
@@ -1537,6 +1558,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
         if (cfg->autoreset && cfg->autoreset_mode == HG_AUTORESET_NEXT_STEP) {   // ov mode's job rings
             if ((err = hipMalloc(&e->ov_recs, sizeof(int4) * 3 * num_envs)) != hipSuccess)
                 return cleanup(err, "hipMalloc ov jobs");
+            if ((err = hipMemset(e->ov_recs, 0xFF, sizeof(int4) * 3 * num_envs)) != hipSuccess)
+                return cleanup(err, "hipMemset ov jobs");
             if ((err = hipMalloc(&e->ov_ring, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc ov ring");
             if ((err = hipMemset(e->ov_ring, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset ov ring");
             e->ov = true;
@@ -1638,7 +1661,8 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
                        e->Pf.env_templates ? e->tmpl_env : nullptr, e->state, e->az, mask, obs, e->n);
     HIP_TRY(hipGetLastError());
     if (e->cfg.reset_mode == HG_RESET_RETRIM) {   // trim each masked env against its last wind (F8)
-        HIP_TRY(hipMemsetAsync(e->retrim_count, 0, sizeof(int32_t), s));
+        int32_t* zero[3] = {e->retrim_count, nullptr, nullptr};
+        HIP_TRY(zero_counts(zero, s));
         hipLaunchKernelGGL(mask_list_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, s, mask, e->n, e->retrim_list,
                            e->retrim_count);
         hgk::RetrimArgs r;
@@ -1654,6 +1678,7 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
         r.obs = obs;
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
+        r.bad_jobs = e->retrim_count + 2;
         HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), s));
         HIP_TRY(hipGetLastError());
     }
@@ -1692,7 +1717,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     } else {
         e->chain_expect = kChainBroken;
     }
-    if (zero_count) HIP_TRY(hipMemsetAsync(reset_count, 0, sizeof(int32_t), s));
+    int32_t* zero[3] = {zero_count ? reset_count : nullptr, nullptr, nullptr};
     int32_t* rt_count = nullptr;
     int32_t rt_slot = -1;
     const bool ov = retrim && e->ov && e->ov_enabled;
@@ -1707,11 +1732,12 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         rt_count = e->retrim_ring + rt_slot;
         ++e->retrim_gen;
         if (e->retrim_chain != key || eager_after_capture) {
-            HIP_TRY(hipMemsetAsync(rt_count, 0, sizeof(int32_t), s));
-            if (ov) HIP_TRY(hipMemsetAsync(e->ov_ring + rt_slot, 0, sizeof(int32_t), s));
+            zero[1] = rt_count;
+            if (ov) zero[2] = e->ov_ring + rt_slot;
         }
         e->retrim_chain = key;
     }
+    HIP_TRY(zero_counts(zero, s));
     StepArgs a;
     a.hmap = e->hmap;
     a.actions = actions;
@@ -1751,6 +1777,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.obs = obs;
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
+        r.bad_jobs = e->retrim_count + 2;
         r.ov = 1;
         r.tmpl = reinterpret_cast<const float*>(e->tmpl_dev);
         r.tmpl_env = e->Pf.env_templates ? e->tmpl_env : nullptr;
@@ -1772,6 +1799,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.obs = obs;
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
+        r.bad_jobs = e->retrim_count + 2;
         HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), s));
     }
     HIP_TRY(hipGetLastError());
@@ -1921,6 +1949,47 @@ int32_t hg_retrim_failures(hg_env* e, int64_t* count) {
     int32_t v = 0;
     HIP_TRY(hipMemcpy(&v, e->retrim_count + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
     *count = v;
+    return HG_OK;
+}
+
+int32_t hg_debug_retrim_invalid(hg_env* e, int64_t* count) {
+    if (!e || !count) return fail(HG_E_INVALID, "bad env or count");
+    DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
+    int32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, e->retrim_count + 2, sizeof(int32_t), hipMemcpyDeviceToHost));
+    *count = v;
+    return HG_OK;
+}
+
+#if HG_RT_DEBUG
+int hg_debug_rt_log_ov(void* dst, int64_t bytes, int32_t clear) {
+    if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(hgk::g_rt_dbg), (size_t)bytes) != hipSuccess) return -1;
+    unsigned n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(hgk::g_rt_dbg_n), sizeof(n)) != hipSuccess) return -1;
+    if (clear) {
+        const unsigned z = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(hgk::g_rt_dbg_n), &z, sizeof(z));
+    }
+    return (int)n;
+}
+int hg_debug_ptrs(hg_env* e, int64_t* out) {
+    out[0] = (int64_t)(uintptr_t)e->retrim_ring;
+    out[1] = (int64_t)(uintptr_t)e->retrim_count;
+    out[2] = (int64_t)(uintptr_t)e->ov_ring;
+    return 0;
+}
+#endif
+
+int32_t hg_debug_queues(hg_env* e, int32_t* out) {
+    if (!e || !out) return fail(HG_E_INVALID, "bad env or out");
+    DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
+    HIP_TRY(hipDeviceSynchronize());
+    for (int k = 0; k < 9; ++k) out[k] = -7;
+    HIP_TRY(hipMemcpy(out, e->retrim_ring, 3 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (e->ov_ring) HIP_TRY(hipMemcpy(out + 3, e->ov_ring, 3 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(out + 6, e->retrim_count, 3 * sizeof(int32_t), hipMemcpyDeviceToHost));
     return HG_OK;
 }
 

@@ -78,6 +78,7 @@ struct RetrimArgs {
     int32_t ov;
     const float* tmpl;      // ov: the shared reset template (heli 18 | carry 4 | obs 17) ...
     const float* tmpl_env;  // ... or the per-env ones [N][39] (Params::env_templates), else NULL
+    int32_t* bad_jobs;      // env mode: job records naming no env (or a count past N), skipped and counted
 };
 
 // Launch retrim_kernel (one 64-lane block per trim, up to `grid` blocks looping over the jobs).

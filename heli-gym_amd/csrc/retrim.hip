@@ -34,6 +34,19 @@ extern "C" int hg_debug_retrim_timing(void* dst, int64_t bytes) {
 }
 #endif
 
+#if HG_RT_DEBUG
+extern "C" int hg_debug_rt_log_serial(void* dst, int64_t bytes, int32_t clear) {
+    if (dst && hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_rt_dbg), (size_t)bytes) != hipSuccess) return -1;
+    unsigned n = 0;
+    if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_rt_dbg_n), sizeof(n)) != hipSuccess) return -1;
+    if (clear) {
+        const unsigned z = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_rt_dbg_n), &z, sizeof(z));
+    }
+    return (int)n;
+}
+#endif
+
 hipError_t launch_retrim(const RetrimArgs& a, unsigned grid, hipStream_t stream) {
     hipLaunchKernelGGL(retrim_kernel, dim3(grid), dim3(64), 0, stream, a);
     return hipGetLastError();

@@ -149,6 +149,42 @@ __device__ __forceinline__ void gj_steps(double (&A)[16], double& b, uint32_t& l
     if constexpr (C < 15) gj_steps<C + 1>(A, b, live, mycol, i, myinv, sRow, l);
 }
 
+// HG_GJ_SPLIT: the same solve with the four copies of a row splitting its columns.  Lane l holds row
+// i = l & 15 and, in quarter q = l >> 4, the columns 4 jj + q (jj = 0..3) plus the right-hand side
+// (identical in every quarter).  Pivot step C reads column C in quarter C & 3 (each quarter is one DPP
+// row, so the 16-lane max is per quarter and the ballot takes that quarter's 16 bits); the row's
+// multiplier goes to its four quarters and each quarter fetches its own columns of the pivot row with
+// one lane shuffle per column.  Same pivots, same fused operations, so the same results bit for bit,
+// with a quarter of the elementwise work and of the LDS reads per lane.
+#ifndef HG_GJ_SPLIT
+#define HG_GJ_SPLIT 1
+#endif
+template <int C>
+__device__ __forceinline__ void gjs_step(double (&A4)[4], double& b, uint32_t& live, int& mycol, int i, int l) {
+    constexpr int qc = C & 3, jc = C >> 2;
+    const double v = A4[jc];   // column C in quarter qc
+    const uint32_t key = ((uint32_t)(__double_as_longlong(v) >> 32) | 0x80000000u) & live;
+    const double own_inv = rcp_f64(v);
+    const uint32_t mx = row16_max(key);
+    const uint32_t hit = (uint32_t)(__ballot(key == mx) >> (16 * qc)) & 0xFFFFu;
+    const int P = __builtin_ctz(hit | 0x10000u);
+    const double rinv = read_lane(own_inv, 16 * qc + P);
+    const bool piv = i == P;
+    const double g = __shfl(piv ? 0.0 : v * rinv, 16 * qc + i);   // row i's multiplier, from quarter qc
+    const double m = piv ? rinv : 1.0;
+    const int src = (l & 48) + P;   // this quarter's lane of the pivot row
+#pragma unroll
+    for (int jj = jc; jj < 4; ++jj) A4[jj] = fma(-g, __shfl(A4[jj], src), A4[jj] * m);
+    b = fma(-g, read_lane(b, P), b * m);
+    live = piv ? 0u : live;
+    mycol = piv ? C : mycol;
+}
+template <int C>
+__device__ __forceinline__ void gjs_steps(double (&A4)[4], double& b, uint32_t& live, int& mycol, int i, int l) {
+    gjs_step<C>(A4, b, live, mycol, i, l);
+    if constexpr (C < 15) gjs_steps<C + 1>(A4, b, live, mycol, i, l);
+}
+
 // What the observation needs from one evaluation beyond the state: power, uvw_air, ned velocity
 // (observe(), helicopter_dynamics.py:471-488).
 struct EvalExt {
@@ -267,6 +303,10 @@ __device__ __forceinline__ const T& opaque_const(const T* p) {
 #ifndef HG_RETRIM_WAVES
 #define HG_RETRIM_WAVES 2
 #endif
+#if HG_RT_DEBUG
+__device__ long long g_rt_dbg[4096][4];
+__device__ unsigned g_rt_dbg_n;
+#endif
 // The jobs first, first + stride, ... of a batch, one wave (this block) per trim: retrim_kernel and the
 // trim blocks of the overlapped next-step re-trim (heligym_amd.hip step_ov_kernel).
 __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, int64_t stride) {
@@ -284,10 +324,28 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     // <= min(n, 1024)), so the start waits for one load, not two dependent ones
     const int4 rec0 = a.recs ? a.recs[first] : make_int4(0, 0, 0, 0);
     int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
-    if (a.count && jobs > a.n) jobs = a.n;   // a queue holds at most one job per env
+#if HG_RT_DEBUG
+    if (l == 0 && first == 0) {   // diagnostic build: one record per launch (count address, jobs, mode, first record)
+        const unsigned k = atomicAdd(&g_rt_dbg_n, 1u);
+        if (k < 4096) {
+            g_rt_dbg[k][0] = (long long)(uintptr_t)a.count;
+            g_rt_dbg[k][1] = jobs;
+            g_rt_dbg[k][2] = a.ov + (a.list ? 2 : 0) + (a.recs ? 4 : 0);
+            g_rt_dbg[k][3] = rec0.x;
+        }
+    }
+#endif
+    if (a.count && jobs > a.n) {   // a queue holds at most one job per env
+        if (first == 0 && l == 0 && a.bad_jobs) atomicAdd(a.bad_jobs, 1);
+        jobs = a.n;
+    }
     for (int64_t job = first; job < jobs; job += stride) {   // uniform per wave
         const int4 rec = a.recs ? (job == first ? rec0 : a.recs[job]) : make_int4(0, 0, 0, 0);
         const int64_t env = a.recs ? (int64_t)rec.x : (a.list ? (int64_t)a.list[job] : job);
+        if ((a.recs || a.list) && (uint64_t)env >= (uint64_t)a.n) {   // never index the state with a bad record
+            if (l == 0 && a.bad_jobs) atomicAdd(a.bad_jobs, 1);
+            continue;
+        }
         const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];
         double W[3] = {P.wm[0], P.wm[1], P.wm[2]};   // NULL wind: the mean wind (helicopter.py:55)
         if (a.recs) {
@@ -377,6 +435,32 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             }
             lds_order();
             RSTAMP(3 + 4 * round, "v"(ye[0]));
+#if HG_GJ_SPLIT
+            {
+                const int i = l & 15, q = l >> 4;
+                double A4[4], Em4[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {   // all 9 reads issued before the first use
+                    A4[jj] = sE[(4 * jj + q) * 16 + i];
+                    Em4[jj] = sE[(4 * jj + q + 16) * 16 + i];
+                }
+                double b = sR[i];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) A4[jj] = (A4[jj] - Em4[jj]) * (0.5 / eps);
+                uint32_t live = 0xFFFFFFFFu;
+                int mycol = 0;
+                gjs_steps<0>(A4, b, live, mycol, i, l);
+                if (l < 16) sX[mycol] = b;
+                lds_order();
+                bool fin = true;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    dir[k] = sX[k];
+                    fin = fin && isfinite(dir[k]);
+                }
+                if (!fin) { ok = false; break; }
+            }
+#else
             {
                 const int i = l & 15;
                 double A[16], Em[16];
@@ -402,6 +486,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                 }
                 if (!fin) { ok = false; break; }
             }
+#endif
             RSTAMP(4 + 4 * round, "v"(dir[0]));
             kind = kRoundNormal;
             ++round;

@@ -106,6 +106,8 @@ _SIGS = {
     "hg_trim_batch": (ctypes.c_int32, [_P, _P, ctypes.c_int64, _P, _P, _P, _P, _P]),
     "hg_retrim_failures": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "hg_set_retrim_overlap": (ctypes.c_int32, [_P, ctypes.c_int32]),
+    "hg_debug_retrim_invalid": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "hg_debug_queues": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int32)]),
     "hg_trim_conds_batch": (ctypes.c_int32, [_P, ctypes.POINTER(hg_trim_cond), ctypes.c_int64, _P, _P, _P, _P,
                                              _P, _P]),
     "hg_set_reset_templates": (ctypes.c_int32, [_P, _P, _P]),

@@ -599,6 +599,12 @@ class HeliVecEnv(*_VEC_BASES):
         self._check(self.lib.hg_retrim_failures(self._h, ctypes.byref(c)))
         return c.value
 
+    def retrim_invalid_jobs(self):
+        """Diagnostic: re-trim job records that named no env (skipped); 0 in a correct run."""
+        c = ctypes.c_int64()
+        self._check(self.lib.hg_debug_retrim_invalid(self._h, ctypes.byref(c)))
+        return c.value
+
     def random_actions(self, out, seed, step, lo=-1.0, hi=1.0):
         self._check(self.lib.hg_random_actions(self._h, _ptr(out), int(seed), int(step), float(lo),
                                                float(hi), self._stream()))

@@ -294,6 +294,14 @@ int32_t hg_load_specialized(hg_env* env, const char* code_object_path, int32_t t
  * Synchronises with the device. */
 int32_t hg_retrim_failures(hg_env* env, int64_t* count);
 
+/* Diagnostic: re-trim job records that named no env (or a job count past N), skipped by the trim
+ * instead of indexing the state with them; 0 in a correct run.  Synchronises with the device. */
+int32_t hg_debug_retrim_invalid(hg_env* env, int64_t* count);
+
+/* Diagnostic: the re-trim job-count rings (out[0..2] the step re-trim ring, out[3..5] the overlapped
+ * re-trim ring or -7, out[6..8] hg_reset's job count, failures, invalid jobs).  Synchronises. */
+int32_t hg_debug_queues(hg_env* env, int32_t* out);
+
 /* HG_RESET_RETRIM with next-step auto-reset (gymnasium's default, make_vec's): the episodes a step ends
  * are re-trimmed (helicopter.py:208-212 -> helicopter_dynamics.py:491-555) while the next step runs,
  * in the same kernel launch as that step (its first blocks), so the caller's stream sees every step

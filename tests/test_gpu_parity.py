@@ -917,6 +917,42 @@ def test_retrim_overlap_bitwise_equals_serial(torch, graph_steps):
         np.testing.assert_array_equal(x, y, err_msg=f"output {j}")
 
 
+@pytest.mark.parametrize("mode", ["same_step", "next_step"])
+def test_retrim_graph_replays_keep_job_counts(torch, mode):
+    """reset_mode="retrim" graph-replayed back to back, get_state between replays (the bench's timed
+    windows): every re-trim reads the job count its step wrote, so no trim ever meets a job record its
+    step did not write (hg_debug_retrim_invalid).  Round 4 regression: the counters were zeroed by a
+    captured 4-byte hipMemsetAsync, which on MI355X left them stale on later replays; the trim then
+    read records past the step's own and faulted on the never-written ones."""
+    N, B = 65536, 50
+    env = make_env(torch, N, "hover", 0.01, autoreset=True, reset_mode="retrim", autoreset_mode=mode, seed=1234)
+    env.reset()
+    bank = torch.empty((B, N, 4), dtype=torch.float32, device=env.device)
+    for k in range(B):
+        env.random_actions(bank[k], seed=0x5EED, step=k)
+    bank[:, ::5, 0] = -1.0   # low collective on every fifth env: crashes and resets throughout
+    for k in range(400):
+        env.step_async(bank[k % B], with_reset_info=False)
+    s = torch.cuda.Stream(device=env.device)
+    s.wait_stream(torch.cuda.current_stream(env.device))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for k in range(B):
+            env.step_async(bank[k], with_reset_info=False)
+    e0 = int(env.get_state()[1][:, 2].long().sum())
+    for r in range(8):
+        g.replay()
+        if r % 2:
+            env.get_state()
+    torch.cuda.synchronize()
+    e1 = int(env.get_state()[1][:, 2].long().sum())
+    assert e1 - e0 > 1000, (e0, e1)   # re-trimmed resets in the replays
+    assert env.retrim_invalid_jobs() == 0
+    assert env.retrim_failures() == 0
+    del g
+    env.close()
+
+
 def test_make_vec_registry_defaults(torch):
     import heligym_amd
     env = heligym_amd.make_vec("HeliHover-v0", 64, dt=0.02)
