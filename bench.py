@@ -277,27 +277,28 @@ class Timer:
         t = self.torch
         s = stream if stream is not None else t.cuda.current_stream(self.dev)
         secs, walls, resets = [], [], 0
+        inner = isinstance(body, TimedGraph)   # the events are inside the body's graph
         for _ in range(repeats):
             if self.world > 1:
                 self.dist.barrier()
             t.cuda.synchronize()
             e0, e1 = t.cuda.Event(enable_timing=True), t.cuda.Event(enable_timing=True)
-            if preroll:
+            if preroll and not inner:
                 getattr(body, "preroll", body)()
-            n0 = episodes(env, sync=False) if env is not None else None
+            n0 = episodes(env, sync=False) if env is not None and not inner else None
             w0 = time.perf_counter()
             e0.record(s)
             body()
             e1.record(s)
             w1 = time.perf_counter()
-            n1 = episodes(env, sync=False) if env is not None else None
+            n1 = episodes(env, sync=False) if env is not None and not inner else None
             t.cuda.synchronize()
             if self.world > 1:
                 self.dist.barrier()
             walls.append(max(time.perf_counter(), w1) - w0)
-            secs.append(e0.elapsed_time(e1) * 1e-3)
+            secs.append(body.inner_s() if inner else e0.elapsed_time(e1) * 1e-3)
             if env is not None:
-                resets += int(n1) - int(n0)
+                resets += body.resets() if inner else int(n1) - int(n0)
         v = t.tensor(secs + walls, dtype=t.float64, device=self.dev)
         self.per_rank = [statistics.median(secs)]
         if self.world > 1:
@@ -326,6 +327,140 @@ def progress(msg):
     """One line per bench phase on stderr (the JSON line stays the last line of stdout): a run that
     fails names the phase it failed in."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+class _Hip:
+    """The HIP runtime through ctypes, for what torch does not expose on ROCm: timing events recorded
+    by event-record nodes of an explicitly built hipGraph (torch refuses external events on ROCm)."""
+    lib = None
+
+    @classmethod
+    def get(cls):
+        if cls.lib is None:
+            import ctypes
+            cls.lib = ctypes.CDLL("libamdhip64.so")
+        return cls.lib
+
+
+def _hip_ok(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what}: hipError {rc}")
+
+
+class TimedGraph:
+    """One hipGraph: a pre-roll of B steps, the episode count, HIP event e0, exactly K steps, HIP event
+    e1, the episode count again (each part a captured child graph, the events event-record nodes).
+    The events bracket the K timed steps only, so a window of any K measures steps in steady state:
+    the GPU is already stepping when e0 is recorded and no launch latency of the window's own start
+    falls inside it (a short window measured as its own graph or eager launches includes about 8 us
+    of graph-launch or host latency).  `inner_s()` is the K steps' time, `resets()` the episodes begun
+    in them (device scalars read after a synchronize)."""
+
+    def __init__(self, torch, dev, one_step, K, B, env=None):
+        import ctypes
+        self.torch, self.K = torch, K
+        hip = _Hip.get()
+        self.ctypes = ctypes
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for k in range(B):   # warm the capture stream
+                one_step(k)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize()
+        self.n = [None, None]
+
+        def cap(fn):
+            g = torch.cuda.CUDAGraph(keep_graph=True)
+            with torch.cuda.graph(g, stream=s):
+                fn()
+            return g
+
+        def count(j):
+            def f():
+                if env is not None and hasattr(env, "get_state"):
+                    _, c = env.get_state()
+                    self.n[j] = c[:, 2].long().sum()
+                else:   # (an empty child graph is not allowed)
+                    self.n[j] = torch.zeros((), dtype=torch.int64, device=dev) + 0
+            return f
+        self.parts = [cap(lambda: [one_step(k) for k in range(B)]), cap(count(0)),
+                      cap(lambda: [one_step(k % B) for k in range(K)]), cap(count(1))]
+        self.ev = []
+        for _ in range(2):
+            h = ctypes.c_void_p()
+            _hip_ok(hip.hipEventCreate(ctypes.byref(h)), "hipEventCreate")
+            self.ev.append(h)
+        self.graph = ctypes.c_void_p()
+        _hip_ok(hip.hipGraphCreate(ctypes.byref(self.graph), ctypes.c_uint(0)), "hipGraphCreate")
+        prev = None
+        order = [("g", self.parts[0]), ("g", self.parts[1]), ("e", self.ev[0]), ("g", self.parts[2]),
+                 ("e", self.ev[1]), ("g", self.parts[3])]
+        for kind, obj in order:
+            node = ctypes.c_void_p()
+            deps = (ctypes.c_void_p * 1)(prev) if prev is not None else None
+            nd = ctypes.c_size_t(0 if prev is None else 1)
+            if kind == "g":
+                _hip_ok(hip.hipGraphAddChildGraphNode(ctypes.byref(node), self.graph, deps, nd,
+                                                      ctypes.c_void_p(obj.raw_cuda_graph())), "child graph node")
+            else:
+                _hip_ok(hip.hipGraphAddEventRecordNode(ctypes.byref(node), self.graph, deps, nd, obj),
+                        "event record node")
+            prev = node
+        self.exec = ctypes.c_void_p()
+        _hip_ok(hip.hipGraphInstantiate(ctypes.byref(self.exec), self.graph, None, None, ctypes.c_size_t(0)),
+                "hipGraphInstantiate")
+        self()
+        torch.cuda.synchronize()
+        self.inner_s()   # the events work (raises otherwise)
+
+    def __call__(self):
+        st = self.ctypes.c_void_p(self.torch.cuda.current_stream().cuda_stream)
+        _hip_ok(_Hip.get().hipGraphLaunch(self.exec, st), "hipGraphLaunch")
+
+    def inner_s(self):
+        ms = self.ctypes.c_float()
+        _hip_ok(_Hip.get().hipEventElapsedTime(self.ctypes.byref(ms), self.ev[0], self.ev[1]), "hipEventElapsedTime")
+        return ms.value * 1e-3
+
+    def resets(self):
+        return int(self.n[1].item()) - int(self.n[0].item())
+
+    def close(self):
+        if getattr(self, "exec", None) is None:
+            return
+        hip = _Hip.get()
+        self.torch.cuda.synchronize()
+        hip.hipGraphExecDestroy(self.exec)
+        hip.hipGraphDestroy(self.graph)
+        for h in self.ev:
+            hip.hipEventDestroy(h)
+        self.exec = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def windows(torch, dev, one_step, K, B, env=None):
+    """The timed body for exactly K steps: a TimedGraph (events inside the graph around the K steps),
+    or -- where the explicit graph API is unavailable -- graphs_for's replays.  Returns (body, keep,
+    mode)."""
+    if os.environ.get("HG_BENCH_OUTER_WINDOWS") != "1":
+        try:
+            tg = TimedGraph(torch, dev, one_step, K, B, env)
+            return tg, (tg,), f"one hipGraph per window: {B} pre-roll steps, then the {K} timed steps between HIP events"
+        except Exception as exc:   # (reported in the mode string)
+            torch.cuda.synchronize()
+            progress(f"TimedGraph unavailable ({exc}); graph replays")
+            err = f" (TimedGraph unavailable: {exc})"
+    else:
+        err = ""
+    rep, keep = graphs_for(torch, dev, one_step, K, B)
+    return rep, keep, (f"hipGraphs of {B} steps" + (f" + {K % B} eager launches" if K % B else "") if K >= B
+                       else f"{K} eager launches behind a queued {B}-step hipGraph") + err
 
 
 def graphs_for(torch, dev, one_step, K, B):
@@ -520,13 +655,13 @@ def airframes(args, torch, timer, N, dev, B, K, R, head_s):
 
         def one(k):
             env.step_async(bank[k % B], with_reset_info=False)
-        rep, keep = graphs_for(torch, dev, one, K, B)
+        rep, keep, _m = windows(torch, dev, one, K, B, env)
         s_g, _, _, rs_g = timer.run_counted(env, rep, R)
         del keep
         t0 = time.perf_counter()
         spec = env.specialize()
         t_build = time.perf_counter() - t0
-        rep, keep = graphs_for(torch, dev, one, K, B)
+        rep, keep, _m = windows(torch, dev, one, K, B, env)
         s_s, _, _, rs_s = timer.run_counted(env, rep, R)
         del keep
         out[name] = {"generic_ms_per_step": s_g / K * 1e3, "specialised_ms_per_step": s_s / K * 1e3,
@@ -566,7 +701,7 @@ def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev
             for k in range(K5):
                 step5(k)
     else:
-        rep5, _k5 = graphs_for(torch, dev, step5, K5, B)
+        rep5, _k5, _m5 = windows(torch, dev, step5, K5, B, env5)
     s_n5, _, _, rs_n5 = timer.run_counted(env5, rep5, R)
     ranks_n5 = timer.per_rank
     return {"workload": f"HeliHover-v0 x {CONFIG5_TOTAL} envs sharded over {world} ranks ({n5} on rank {rank})",
@@ -680,11 +815,11 @@ def main():
                 for k in range(K):
                     one_step(k)
         else:
-            replay, _keep = graphs_for(torch, dev, one_step, K, B)
+            replay, _keep, mode = windows(torch, dev, one_step, K, B, env)
         sec, secs, wall, resets = timer.run_counted(env, replay, R)
         per_rank = timer.per_rank
-        mode = (f"hipGraphs of {B} steps" + (f" + {K % B} eager launches" if K % B else "") if K >= B
-                else f"{K} eager launches behind a queued {B}-step hipGraph")
+        if args.dry_run:
+            mode = f"{K} eager launches (dry run)"
         total_envs = N * world
 
         if not args.no_secondary and not args.dry_run:
@@ -695,7 +830,7 @@ def main():
 
                 def one_step_ri(k):
                     env.step_async(bank[k % B], with_reset_info=True)
-                rep_ri, _k2 = graphs_for(torch, dev, one_step_ri, K, B)
+                rep_ri, _k2, _m = windows(torch, dev, one_step_ri, K, B, env)
                 s_ri, _, _, rs_ri = timer.run_counted(env, rep_ri, R)
                 del _k2
                 secondary["step_with_reset_info"] = {
@@ -722,7 +857,7 @@ def main():
                 # the generic kernel (model constants loaded, any airframe); bitwise-identical results
                 progress("generic_kernel")
                 env.set_specialized(False)
-                rep_g, _k3 = graphs_for(torch, dev, one_step, K, B)
+                rep_g, _k3, _m = windows(torch, dev, one_step, K, B, env)
                 s_g, _, _, rs_g = timer.run_counted(env, rep_g, R)
                 del _k3
                 env.set_specialized(True)
@@ -758,11 +893,11 @@ def main():
             # the same workload with exact F8 resets: every auto-reset re-trimmed on the device against
             # the env's last wind (reset_mode="retrim", helicopter.py:208-212)
             Kr = min(K, 500)
-            for name, mode in (("retrim", args.autoreset_mode), ("retrim_next_step", "next_step")):
+            for name, amode in (("retrim", args.autoreset_mode), ("retrim_next_step", "next_step")):
                 if name == "retrim_next_step" and args.autoreset_mode == "next_step":
                     continue
-                progress(f"{name} ({mode})")
-                envr = make_env(argparse.Namespace(**{**vars(args), "reset_mode": "retrim", "autoreset_mode": mode}),
+                progress(f"{name} ({amode})")
+                envr = make_env(argparse.Namespace(**{**vars(args), "reset_mode": "retrim", "autoreset_mode": amode}),
                                 torch, N, rank * N, dev)
 
                 def stepr(k):
@@ -770,15 +905,15 @@ def main():
                 aged_r = age(args, torch, envr, bank, B)
                 for k in range(min(args.warmup, 50)):
                     stepr(k)
-                repr_, _kr = graphs_for(torch, dev, stepr, Kr, B)
+                repr_, _kr, _m = windows(torch, dev, stepr, Kr, B, envr)
                 s_rt, _, _, rs_rt = timer.run_counted(envr, repr_, 3)
                 del _kr
-                ov = mode == "next_step" and envr.set_retrim_overlap(True)
+                ov = amode == "next_step" and envr.set_retrim_overlap(True)
                 # a window without a reset would time the plain step, not the re-trim: no value then
                 secondary[name] = {
                     "envs": N, "value": N * Kr / s_rt if rs_rt > 0 else None, "unit": "env-steps/s",
                     "ms_per_step": s_rt / Kr * 1e3 if rs_rt > 0 else None, "window_ms_per_step": s_rt / Kr * 1e3,
-                    "resets_in_window": rs_rt, "aged_steps": aged_r, "autoreset_mode": mode,
+                    "resets_in_window": rs_rt, "aged_steps": aged_r, "autoreset_mode": amode,
                     "steps": Kr, "retrim_failures": envr.retrim_failures(),
                     "retrim_invalid_jobs": envr.retrim_invalid_jobs(),
                     "note": "reset_mode='retrim': each auto-reset re-trimmed on the device (Newton trim against the "
@@ -801,7 +936,7 @@ def main():
             aged_x = age(args, torch, envx, bankx, B)
             for k in range(min(args.warmup, 20)):
                 stepx(k)
-            repx, _kx = graphs_for(torch, dev, stepx, Kx, B)
+            repx, _kx, _m = windows(torch, dev, stepx, Kx, B, envx)
             s_x, _, _, rs_x = timer.run_counted(envx, repx, 3)
             del _kx
             ach = Nx * BYTES_PER_ENV_STEP / (s_x / Kx) / 1e9

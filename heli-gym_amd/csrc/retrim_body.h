@@ -157,7 +157,7 @@ __device__ __forceinline__ void gj_steps(double (&A)[16], double& b, uint32_t& l
 // one lane shuffle per column.  Same pivots, same fused operations, so the same results bit for bit,
 // with a quarter of the elementwise work and of the LDS reads per lane.
 #ifndef HG_GJ_SPLIT
-#define HG_GJ_SPLIT 1
+#define HG_GJ_SPLIT 2
 #endif
 template <int C>
 __device__ __forceinline__ void gjs_step(double (&A4)[4], double& b, uint32_t& live, int& mycol, int i, int l) {
@@ -183,6 +183,43 @@ template <int C>
 __device__ __forceinline__ void gjs_steps(double (&A4)[4], double& b, uint32_t& live, int& mycol, int i, int l) {
     gjs_step<C>(A4, b, live, mycol, i, l);
     if constexpr (C < 15) gjs_steps<C + 1>(A4, b, live, mycol, i, l);
+}
+
+// HG_GJ_SPLIT 2: as 1, and the next three pivot columns (C, C+1, C+2) also replicated in every quarter
+// (rep, nx1, nx2), so that a pivot step's chain -- search, reciprocal, multiplier, the update of
+// the next pivot column -- has no lane shuffle in it: the multiplier is formed in every quarter and
+// the next column is updated with a readlane of the pivot row's value.  The owners keep their columns
+// from C+3 on current (one shuffle per column, off that chain), and column C+3 is broadcast to the
+// quarters at the end of step C.  The same values in the same operations: bitwise the solve above.
+template <int C>
+__device__ __forceinline__ void gjr_step(double (&A4)[4], double& b, double& rep, double& nx1, double& nx2,
+                                         uint32_t& live, int& mycol, int i, int l) {
+    const uint32_t key = ((uint32_t)(__double_as_longlong(rep) >> 32) | 0x80000000u) & live;
+    const double own_inv = rcp_f64(rep);
+    const uint32_t mx = row16_max(key);
+    const uint32_t hit = (uint32_t)__ballot(key == mx) & 0xFFFFu;
+    const int P = __builtin_ctz(hit | 0x10000u);
+    const double rinv = read_lane(own_inv, P);
+    const bool piv = i == P;
+    const double g = piv ? 0.0 : rep * rinv;
+    const double m = piv ? rinv : 1.0;
+    if constexpr (C + 1 < 16) nx1 = fma(-g, read_lane(nx1, P), nx1 * m);
+    if constexpr (C + 2 < 16) nx2 = fma(-g, read_lane(nx2, P), nx2 * m);
+    const int src = (l & 48) + P;
+#pragma unroll
+    for (int jj = (C + 3) >> 2; jj < 4; ++jj) A4[jj] = fma(-g, __shfl(A4[jj], src), A4[jj] * m);
+    b = fma(-g, read_lane(b, P), b * m);
+    live = piv ? 0u : live;
+    mycol = piv ? C : mycol;
+    rep = nx1;
+    nx1 = nx2;
+    if constexpr (C + 3 < 16) nx2 = __shfl(A4[(C + 3) >> 2], 16 * ((C + 3) & 3) + i);
+}
+template <int C>
+__device__ __forceinline__ void gjr_steps(double (&A4)[4], double& b, double& rep, double& nx1, double& nx2,
+                                          uint32_t& live, int& mycol, int i, int l) {
+    gjr_step<C>(A4, b, rep, nx1, nx2, live, mycol, i, l);
+    if constexpr (C < 15) gjr_steps<C + 1>(A4, b, rep, nx1, nx2, live, mycol, i, l);
 }
 
 // What the observation needs from one evaluation beyond the state: power, uvw_air, ned velocity
@@ -449,7 +486,14 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                 for (int jj = 0; jj < 4; ++jj) A4[jj] = (A4[jj] - Em4[jj]) * (0.5 / eps);
                 uint32_t live = 0xFFFFFFFFu;
                 int mycol = 0;
+#if HG_GJ_SPLIT == 2
+                double rep = (sE[i] - sE[16 * 16 + i]) * (0.5 / eps);
+                double nx1 = (sE[16 + i] - sE[17 * 16 + i]) * (0.5 / eps);
+                double nx2 = (sE[32 + i] - sE[18 * 16 + i]) * (0.5 / eps);
+                gjr_steps<0>(A4, b, rep, nx1, nx2, live, mycol, i, l);
+#else
                 gjs_steps<0>(A4, b, live, mycol, i, l);
+#endif
                 if (l < 16) sX[mycol] = b;
                 lds_order();
                 bool fin = true;
