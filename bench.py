@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=1000, help="steps per timed window (exactly)")
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--repeats", type=int, default=5, help="timed windows; the median is reported")
-    ap.add_argument("--age-seconds", type=float, default=30.0,
+    ap.add_argument("--age-seconds", type=float, default=60.0,
                     help="simulated seconds every env population is stepped (untimed, after reset) before its "
                          "graphs are captured, so that timed windows see steady-state episode phases and resets")
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
@@ -272,12 +272,13 @@ class Timer:
     def __init__(self, torch, dist, world, dev):
         self.torch, self.dist, self.world, self.dev = torch, dist, world, dev
         self.per_rank = None   # the last run's median window of every rank (before the max)
+        self.event_s = None
 
     def run(self, body, repeats, stream=None, env=None, preroll=True):
         t = self.torch
         s = stream if stream is not None else t.cuda.current_stream(self.dev)
-        secs, walls, resets = [], [], 0
-        inner = isinstance(body, TimedGraph)   # the events are inside the body's graph
+        secs, walls, resets, events = [], [], 0, []
+        inner = isinstance(body, TimedGraph)   # the window's clock stamps are inside the body's graph
         for _ in range(repeats):
             if self.world > 1:
                 self.dist.barrier()
@@ -297,6 +298,8 @@ class Timer:
                 self.dist.barrier()
             walls.append(max(time.perf_counter(), w1) - w0)
             secs.append(body.inner_s() if inner else e0.elapsed_time(e1) * 1e-3)
+            if inner:
+                events.append(e0.elapsed_time(e1) * 1e-3)
             if env is not None:
                 resets += body.resets() if inner else int(n1) - int(n0)
         v = t.tensor(secs + walls, dtype=t.float64, device=self.dev)
@@ -310,6 +313,8 @@ class Timer:
         v = v.cpu().tolist()
         secs, walls = v[:repeats], v[repeats:]
         self.resets = resets
+        # (TimedGraph) HIP events around each whole graph: pre-roll + counts + the K steps
+        self.event_s = statistics.median(events) if events else None
         return statistics.median(secs), secs, statistics.median(walls)
 
     def run_counted(self, env, body, repeats, stream=None):
@@ -329,38 +334,25 @@ def progress(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-class _Hip:
-    """The HIP runtime through ctypes, for what torch does not expose on ROCm: timing events recorded
-    by event-record nodes of an explicitly built hipGraph (torch refuses external events on ROCm)."""
-    lib = None
-
-    @classmethod
-    def get(cls):
-        if cls.lib is None:
-            import ctypes
-            cls.lib = ctypes.CDLL("libamdhip64.so")
-        return cls.lib
-
-
-def _hip_ok(rc, what):
-    if rc != 0:
-        raise RuntimeError(f"{what}: hipError {rc}")
-
-
 class TimedGraph:
-    """One hipGraph: a pre-roll of B steps, the episode count, HIP event e0, exactly K steps, HIP event
-    e1, the episode count again (each part a captured child graph, the events event-record nodes).
-    The events bracket the K timed steps only, so a window of any K measures steps in steady state:
-    the GPU is already stepping when e0 is recorded and no launch latency of the window's own start
-    falls inside it (a short window measured as its own graph or eager launches includes about 8 us
-    of graph-launch or host latency).  `inner_s()` is the K steps' time, `resets()` the episodes begun
-    in them (device scalars read after a synchronize)."""
+    """One hipGraph per window: a pre-roll of B steps, the episode count, a GPU clock stamp, exactly K
+    steps, a second stamp, the episode count again.  The stamps (hg_clock_stamp: the constant 100 MHz
+    clock, written by a one-lane kernel) bracket the K timed steps, so a window of any K measures them
+    in steady state: the GPU is already stepping when the first stamp is taken, and the window holds K
+    step kernels with their dependent-launch gaps plus the gap after the first stamp (about 1.6 us).
+    HIP events around a short window add about 15 us of event and launch latency to it (20 steps:
+    8.4-8.5 us per step against 7.6-7.7 at 1 000 steps, scripts/r04_batch4.sh), which is why they are
+    not the window's clock here; they still bracket the whole graph (`event_s`, reported beside it).
+    `inner_s()` is the K steps' time, `resets()` the episodes begun in them and the W = 8 untimed
+    steps right before them (the first count sits W steps before the first stamp)."""
 
-    def __init__(self, torch, dev, one_step, K, B, env=None):
+    CLOCK_HZ = 100e6
+
+    def __init__(self, torch, dev, one_step, K, B, env):
         import ctypes
         self.torch, self.K = torch, K
-        hip = _Hip.get()
-        self.ctypes = ctypes
+        lib = env.lib
+        self.stamps = torch.zeros((2,), dtype=torch.int64, device=dev)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
@@ -370,88 +362,60 @@ class TimedGraph:
         torch.cuda.synchronize()
         self.n = [None, None]
 
-        def cap(fn):
-            g = torch.cuda.CUDAGraph(keep_graph=True)
-            with torch.cuda.graph(g, stream=s):
-                fn()
-            return g
-
         def count(j):
-            def f():
-                if env is not None and hasattr(env, "get_state"):
-                    _, c = env.get_state()
-                    self.n[j] = c[:, 2].long().sum()
-                else:   # (an empty child graph is not allowed)
-                    self.n[j] = torch.zeros((), dtype=torch.int64, device=dev) + 0
-            return f
-        self.parts = [cap(lambda: [one_step(k) for k in range(B)]), cap(count(0)),
-                      cap(lambda: [one_step(k % B) for k in range(K)]), cap(count(1))]
-        self.ev = []
-        for _ in range(2):
-            h = ctypes.c_void_p()
-            _hip_ok(hip.hipEventCreate(ctypes.byref(h)), "hipEventCreate")
-            self.ev.append(h)
-        self.graph = ctypes.c_void_p()
-        _hip_ok(hip.hipGraphCreate(ctypes.byref(self.graph), ctypes.c_uint(0)), "hipGraphCreate")
-        prev = None
-        order = [("g", self.parts[0]), ("g", self.parts[1]), ("e", self.ev[0]), ("g", self.parts[2]),
-                 ("e", self.ev[1]), ("g", self.parts[3])]
-        for kind, obj in order:
-            node = ctypes.c_void_p()
-            deps = (ctypes.c_void_p * 1)(prev) if prev is not None else None
-            nd = ctypes.c_size_t(0 if prev is None else 1)
-            if kind == "g":
-                _hip_ok(hip.hipGraphAddChildGraphNode(ctypes.byref(node), self.graph, deps, nd,
-                                                      ctypes.c_void_p(obj.raw_cuda_graph())), "child graph node")
+            _, c = env.get_state()
+            self.n[j] = c[:, 2].long().sum()
+
+        def stamp(j):
+            st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            if lib.hg_clock_stamp(ctypes.c_void_p(self.stamps[j:j + 1].data_ptr()), st) != 0:
+                raise RuntimeError("hg_clock_stamp failed")
+        # layout (A/B, scripts/r04_batch6.sh): 0 the first episode count right before the first stamp;
+        # 1 no counts; 2 (default) W = 8 plain steps between that count and the first stamp -- the
+        # steps right after the count kernels run slower (20-step windows: 8.11 / 8.01 / 7.96 us);
+        # a pre-roll of 1 000 steps instead of 100: 8.17 -> 7.89 us (the GPU's clock and caches settle)
+        layout = int(os.environ.get("HG_TG_LAYOUT", "2"))
+        W = self.W = 8 if layout == 2 else 0
+        P = int(os.environ.get("HG_TG_PREROLL", str(max(B, 1000))))
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=s):
+            for k in range(P - W):
+                one_step(k % B)
+            if layout != 1:
+                count(0)
+            for k in range(P - W, P):
+                one_step(k % B)
+            stamp(0)
+            for k in range(K):
+                one_step(k % B)
+            stamp(1)
+            if layout != 1:
+                count(1)
             else:
-                _hip_ok(hip.hipGraphAddEventRecordNode(ctypes.byref(node), self.graph, deps, nd, obj),
-                        "event record node")
-            prev = node
-        self.exec = ctypes.c_void_p()
-        _hip_ok(hip.hipGraphInstantiate(ctypes.byref(self.exec), self.graph, None, None, ctypes.c_size_t(0)),
-                "hipGraphInstantiate")
+                self.n = [self.stamps[0] * 0, self.stamps[0] * 0]
         self()
         torch.cuda.synchronize()
-        self.inner_s()   # the events work (raises otherwise)
 
     def __call__(self):
-        st = self.ctypes.c_void_p(self.torch.cuda.current_stream().cuda_stream)
-        _hip_ok(_Hip.get().hipGraphLaunch(self.exec, st), "hipGraphLaunch")
+        self.graph.replay()
 
     def inner_s(self):
-        ms = self.ctypes.c_float()
-        _hip_ok(_Hip.get().hipEventElapsedTime(self.ctypes.byref(ms), self.ev[0], self.ev[1]), "hipEventElapsedTime")
-        return ms.value * 1e-3
+        t = self.stamps.tolist()
+        return (t[1] - t[0]) / self.CLOCK_HZ
 
     def resets(self):
         return int(self.n[1].item()) - int(self.n[0].item())
-
-    def close(self):
-        if getattr(self, "exec", None) is None:
-            return
-        hip = _Hip.get()
-        self.torch.cuda.synchronize()
-        hip.hipGraphExecDestroy(self.exec)
-        hip.hipGraphDestroy(self.graph)
-        for h in self.ev:
-            hip.hipEventDestroy(h)
-        self.exec = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
 
 
 def windows(torch, dev, one_step, K, B, env=None):
     """The timed body for exactly K steps: a TimedGraph (events inside the graph around the K steps),
     or -- where the explicit graph API is unavailable -- graphs_for's replays.  Returns (body, keep,
     mode)."""
-    if os.environ.get("HG_BENCH_OUTER_WINDOWS") != "1":
+    if os.environ.get("HG_BENCH_OUTER_WINDOWS") != "1" and env is not None and hasattr(env, "lib"):
         try:
             tg = TimedGraph(torch, dev, one_step, K, B, env)
-            return tg, (tg,), f"one hipGraph per window: {B} pre-roll steps, then the {K} timed steps between HIP events"
+            return tg, (tg,), (f"one hipGraph per window: {B} pre-roll steps, then the {K} timed steps between "
+                               "two GPU clock stamps")
         except Exception as exc:   # (reported in the mode string)
             torch.cuda.synchronize()
             progress(f"TimedGraph unavailable ({exc}); graph replays")
@@ -533,7 +497,9 @@ def age(args, torch, env, bank, B, dt=None):
     """Step a freshly reset population for --age-seconds of simulated time (untimed), so that its
     episodes are spread over their phases -- crashes, gear contact, resets -- as in a long run.
     Every env starts its first episode together; random-action episodes end after about 10 s
-    (SURVEY a27), so without this a short timed window right after reset holds no episode end."""
+    (SURVEY a27), so without this a short timed window right after reset holds no episode end.  The
+    envs that never crash (about 5 %, most of them resting on the ground) reach the 40 s time limit
+    together; the default 60 s ages the population past that cohort (scripts/r04_population.py)."""
     if args.dry_run:
         return 0
     steps = int(round(args.age_seconds / (dt or args.dt)))
@@ -774,6 +740,7 @@ def main():
     R = max(1, args.repeats)
 
     secondary = {}
+    head_event_s = None
     if args.gather_obs:
         # headline = BASELINE config 5: CONFIG5_TOTAL envs sharded over the ranks, gather to rank 0
         from heligym_amd.distributed import shard_bounds
@@ -818,6 +785,7 @@ def main():
             replay, _keep, mode = windows(torch, dev, one_step, K, B, env)
         sec, secs, wall, resets = timer.run_counted(env, replay, R)
         per_rank = timer.per_rank
+        head_event_s = timer.event_s
         if args.dry_run:
             mode = f"{K} eager launches (dry run)"
         total_envs = N * world
@@ -1009,17 +977,23 @@ def main():
                    "parallelism": f"env-shard x{world}", "world_size_seen": seen_world,
                    "backend": backend or "none (1 rank)"},
         "timing": {"repeats": R, "window_s": secs, "median_window_s": sec, "wall_median_s": wall,
-                   "wall_note": "host time from submitting the timed body to its completion; each window is "
-                                "preceded by one untimed run of the same body (GPU busy at the first event)",
+                   "window_clock": ("GPU clock stamps (hg_clock_stamp, 100 MHz) around exactly the K step launches inside "
+                                    "each window's hipGraph, after a pre-roll of the same graph" if head_event_s is not None
+                                    else "HIP events around the window's launches"),
+                   "event_window_s": head_event_s,
+                   "event_note": "HIP events around the whole window graph (pre-roll, episode counts, K steps)",
+                   "wall_note": "host time from submitting the timed body to its completion",
                    "steps_per_window": K, "aged_steps": aged,
                    "aged_note": f"each env population stepped {args.age_seconds:g} simulated s (untimed) after reset "
                                 "before capture: windows see steady-state episode phases",
                    "resets_in_window": resets,
+                   "resets_note": ("episodes begun in the K timed steps and the 8 steps before them"
+                                   if head_event_s is not None else "episodes begun in the K timed steps"),
                    "per_rank_ms_per_step": [x / K * 1e3 for x in per_rank]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": f"step_kernel<{args.task.upper()}>", "kernel_avg_us": kern_s * 1e6,
-                     "kernel_avg_source": "HIP events over the median timed window / launches",
+                     "kernel_avg_source": "the median timed window (GPU clock stamps around its K launches) / K",
                      "bytes_per_env_step": BYTES_PER_ENV_STEP,
                      "impl_bytes_per_env_step": IMPL_BYTES_PER_ENV_STEP,
                      "algorithmic_bytes_per_launch": (total_envs // world) * BYTES_PER_ENV_STEP},

@@ -705,6 +705,14 @@ __global__ __launch_bounds__(kBlock) void mask_list_kernel(const uint8_t* mask, 
     if (take) list[base + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)i;
 }
 
+// hg_clock_stamp: the constant 100 MHz GPU clock at the point of the stream this kernel occupies (the
+// value is moved to a vector register and stored with a vector store)
+__global__ __launch_bounds__(64) void clock_stamp_kernel(uint64_t* dst) {
+    uint64_t t = __builtin_amdgcn_s_memrealtime();
+    asm volatile("" : "+v"(t));
+    if (threadIdx.x == 0) *dst = t;
+}
+
 // Job counters zeroed ahead of the launch that counts into them.  A one-thread kernel, not
 // hipMemsetAsync: captured into a hipGraph, a 4-byte memset node left the counter non-zero on later
 // replays on MI355X (0x08080808 and stale counts in scripts/r04_retrim_fault.py), so the re-trim
@@ -2022,6 +2030,13 @@ int32_t hg_set_state(hg_env* e, const float* state, const int32_t* counters, voi
                        reinterpret_cast<uint32_t*>(e->state), e->az, e->tmpl_dev,
                        e->Pf.env_templates ? e->tmpl_env : nullptr, PARAM_ARG(e), (const uint32_t*)state, counters,
                        e->n);
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_clock_stamp(uint64_t* dst, void* stream) {
+    if (!dst || ((uintptr_t)dst & 7)) return fail(HG_E_INVALID, "hg_clock_stamp: dst must be an 8-byte aligned device pointer");
+    hipLaunchKernelGGL(clock_stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dst);
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }

@@ -28,6 +28,9 @@
 
 #include "physics.h"
 
+#ifndef HG_MID_ANGLE_MRAD   // largest stage attitude increment (mrad) of the long-series angle addition; 0: none
+#define HG_MID_ANGLE_MRAD 250
+#endif
 #ifndef HG_STAGE_FLAG    // diagnostic branch flags (HG_TIMING builds of heligym_amd.hip)
 #define HG_STAGE_FLAG(bit) do { } while (0)
 #endif
@@ -283,7 +286,9 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
     a.a[0] = fma_swn_bx(A0, sd01, A0 * cd01.x);
     a.a[1] = A1 * cd2 + f2{A1.y, -A1.x} * sd2;
     a.a[2] = fma_swn_by(A2, sd01, A2 * cd01.y);
-    // a lane with a larger increment (a tumbling env) takes the full sincos, in a wave-uniform branch
+    // a lane with a larger increment (a tumbling env), in a wave-uniform branch: up to HG_MID_ANGLE_MRAD
+    // the same angle addition with the series of sin d / cos d carried to d^7 / d^8 (truncation below
+    // 6e-11 at 0.25 rad, so a few fp32 ulps like the short series at 0.05), past it the full sincos
     const bool small = m_fabs(d01.x) <= 0.05f && m_fabs(d01.y) <= 0.05f && m_fabs(d2) <= 0.05f;
 #ifndef HG_ISA_HOT   // (analysis builds only: the hot path without its cold branches)
     if (wave_any(!small)) {
@@ -291,11 +296,33 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
     if (false) {
 #endif
         HG_STAGE_FLAG(4);
+#if HG_MID_ANGLE_MRAD > 0
+        constexpr float kMid = HG_MID_ANGLE_MRAD * 1e-3f;   // (NaN increments: neither, the full sincos)
+        const bool mid = m_fabs(d01.x) <= kMid && m_fabs(d01.y) <= kMid && m_fabs(d2) <= kMid;
+        if (!small && mid) {
+            const f2 ms = d01 + (d01 * q01) * (K.c6 + q01 * (1.f / 120.f + q01 * (-1.f / 5040.f)));
+            const f2 mc = 1.f + q01 * (-0.5f + q01 * (K.c24 + q01 * (-1.f / 720.f + q01 * (1.f / 40320.f))));
+            const float ms2 = d2 + (d2 * q2) * (K.c6.x + q2 * (1.f / 120.f + q2 * (-1.f / 5040.f)));
+            const float mc2 = 1.f + q2 * (-0.5f + q2 * (K.c24.x + q2 * (-1.f / 720.f + q2 * (1.f / 40320.f))));
+            a.a[0] = fma_swn_bx(A0, ms, A0 * mc.x);
+            a.a[1] = A1 * mc2 + f2{A1.y, -A1.x} * ms2;
+            a.a[2] = fma_swn_by(A2, ms, A2 * mc.y);
+        }
+        if (wave_any(!mid)) {
+            HG_STAGE_FLAG(8);
+            if (!mid) {
+                a.a[0] = sincos2(pp.x);
+                a.a[1] = sincos2(th);
+                a.a[2] = sincos2(pp.y);
+            }
+        }
+#else
         if (!small) {
             a.a[0] = sincos2(pp.x);
             a.a[1] = sincos2(th);
             a.a[2] = sincos2(pp.y);
         }
+#endif
     }
     return a;
 }

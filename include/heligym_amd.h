@@ -329,6 +329,12 @@ int32_t hg_set_state(hg_env* env, const float* state_dev, const int32_t* counter
 int32_t hg_random_actions(hg_env* env, float* actions_dev, uint64_t seed, uint64_t step,
                           float lo, float hi, void* stream);
 
+/* Benchmark clock: one single-lane kernel on `stream` that writes the GPU's constant 100 MHz clock
+ * (s_memrealtime) to dst_dev[0] when it runs.  Two stamps around K steps launched (or captured) on
+ * the same stream time exactly those K kernels, each with its dependent-launch gap, plus the gap
+ * after the first stamp.  Not part of the reference surface. */
+int32_t hg_clock_stamp(uint64_t* dst_dev, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
