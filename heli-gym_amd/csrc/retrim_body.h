@@ -79,6 +79,10 @@ __device__ __forceinline__ uint32_t row16_max(uint32_t k) {
 #define HG_GJ_LDS 0
 #endif
 constexpr int kRowStride = 18;   // doubles per LDS row (16-byte aligned pairs)
+#ifndef HG_E_STRIDE
+#define HG_E_STRIDE 17
+#endif
+constexpr int kEStride = HG_E_STRIDE;   // doubles per evaluation row of sE
 
 template <int C>
 __device__ __forceinline__ void gj_step(double (&A)[16], double& b, uint32_t& live, int& mycol, int i,
@@ -347,7 +351,9 @@ __device__ unsigned g_rt_dbg_n;
 // The jobs first, first + stride, ... of a batch, one wave (this block) per trim: retrim_kernel and the
 // trim blocks of the overlapped next-step re-trim (heligym_amd.hip step_ov_kernel).
 __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, int64_t stride) {
-    __shared__ double sE[32 * 16];   // the +-eps evaluations E[j][k] of the current Newton step
+    // the +-eps evaluations E[j][k] of the current Newton step, row j (the evaluating lane) at a stride
+    // of kEStride doubles: lane j's 16 writes of a 16-double stride all hit the same two banks
+    __shared__ double sE[32 * kEStride];
     __shared__ double sR[16];        // its right-hand side y - y*
     __shared__ double sX[16];        // the solution (Newton direction), by column
     __shared__ double sExt[7];       // observation terms of the current iterate
@@ -464,7 +470,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             lds_order();   // the previous solve's reads are done
             if (l < 32) {
 #pragma unroll
-                for (int k = 0; k < 16; ++k) sE[l * 16 + k] = ye[k];
+                for (int k = 0; k < 16; ++k) sE[l * kEStride + k] = ye[k];
             }
             if (l == src) {
 #pragma unroll
@@ -478,8 +484,8 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                 double A4[4], Em4[4];
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) {   // all 9 reads issued before the first use
-                    A4[jj] = sE[(4 * jj + q) * 16 + i];
-                    Em4[jj] = sE[(4 * jj + q + 16) * 16 + i];
+                    A4[jj] = sE[(4 * jj + q) * kEStride + i];
+                    Em4[jj] = sE[(4 * jj + q + 16) * kEStride + i];
                 }
                 double b = sR[i];
 #pragma unroll
@@ -487,9 +493,9 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                 uint32_t live = 0xFFFFFFFFu;
                 int mycol = 0;
 #if HG_GJ_SPLIT == 2
-                double rep = (sE[i] - sE[16 * 16 + i]) * (0.5 / eps);
-                double nx1 = (sE[16 + i] - sE[17 * 16 + i]) * (0.5 / eps);
-                double nx2 = (sE[32 + i] - sE[18 * 16 + i]) * (0.5 / eps);
+                double rep = (sE[i] - sE[16 * kEStride + i]) * (0.5 / eps);
+                double nx1 = (sE[kEStride + i] - sE[17 * kEStride + i]) * (0.5 / eps);
+                double nx2 = (sE[2 * kEStride + i] - sE[18 * kEStride + i]) * (0.5 / eps);
                 gjr_steps<0>(A4, b, rep, nx1, nx2, live, mycol, i, l);
 #else
                 gjs_steps<0>(A4, b, live, mycol, i, l);
@@ -510,8 +516,8 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                 double A[16], Em[16];
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {   // all 33 reads issued before the first use
-                    A[q] = sE[q * 16 + i];
-                    Em[q] = sE[(q + 16) * 16 + i];
+                    A[q] = sE[q * kEStride + i];
+                    Em[q] = sE[(q + 16) * kEStride + i];
                 }
                 double b = sR[i];
 #pragma unroll
