@@ -28,6 +28,9 @@
 
 #include "physics.h"
 
+#ifndef HG_GEAR_FACTORED   // 1: the landing-gear loads in factored form (see tail of the stage); 0: per point
+#define HG_GEAR_FACTORED 1
+#endif
 #ifndef HG_MID_ANGLE_MRAD   // largest stage attitude increment (mrad) of the long-series angle addition; 0: none
 #define HG_MID_ANGLE_MRAD 250
 #endif
@@ -450,14 +453,47 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
     }
     // landing gear (:385-398), only where some lane of the wave may touch.  QUIRK: the moment uses
     // the ACCUMULATED force (:397).
-#ifndef HG_ISA_HOT
+#if !defined(HG_ISA_HOT) && !defined(HG_ISA_NOGEAR)
     if (wave_any(z > c.cz)) {
 #else
     if (false) {
 #endif
         HG_STAGE_FLAG(2);
+#ifdef HG_ISA_MARK
+        asm volatile("; GEAR_BEGIN");
+#endif
         const float zh = c.g.zh(z);
         const f2 B22 = B12;
+#if HG_GEAR_FACTORED
+        // Factored: every contact force is fz_i b with b = (-s1, B22) the third DCM column, so the
+        // accumulated force after point i is S_i b (S_i the running sum of the fz), the QUIRK moment
+        // sum_i r_i x (S_i b) = (sum_i S_i r_i) x b, and the contact velocity n2 + b.(omega x r_i) =
+        // n2 + r_i.(b x omega).  The same sums in another order: 4 instead of 12 operations per contact
+        // point for the loads, 3 instead of 9 for the velocity.
+        const float bx = -s1, by = B22.x, bz = B22.y;
+        const float ux = by * r - bz * q, uy = bz * p - bx * r, uz = bx * q - by * p;   // b x omega
+        float S = 0.f, Rx = 0.f, Ry = 0.f, Rz = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi) {
+            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
+            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
+            if (-pzh - P.wl_cg_ft < 0.f) {
+                float ru = rx != 0.f ? rx * ux : 0.f;   // r . (b x omega)
+                ru = ry != 0.f ? fmaf(ry, uy, ru) : ru;
+                ru = rz != 0.f ? fmaf(rz, uz, ru) : ru;
+                const float vel_z = n2 + ru;
+                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
+                // (the first point starts the sums; a zero coordinate of a compiled-in gear point drops
+                // its term, here and above)
+                S = gi == 0 ? fz : S + fz;
+                Rx = rx != 0.f ? (gi == 0 ? S * rx : fmaf(S, rx, Rx)) : Rx;
+                Ry = ry != 0.f ? (gi == 0 ? S * ry : fmaf(S, ry, Ry)) : Ry;
+                Rz = rz != 0.f ? (gi == 0 ? S * rz : fmaf(S, rz, Rz)) : Rz;
+            }
+        }
+        const float Fl0 = S * bx, Fl1 = S * by, Fl2 = S * bz;
+        const float Ml0 = Ry * bz - Rz * by, Ml1 = Rz * bx - Rx * bz, Ml2 = Rx * by - Ry * bx;
+#else
         float Fl0 = 0.f, Fl1 = 0.f, Fl2 = 0.f, Ml0 = 0.f, Ml1 = 0.f, Ml2 = 0.f;
 #pragma unroll
         for (int gi = 0; gi < 3; ++gi) {
@@ -473,11 +509,15 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
                 Ml2 += rx * Fl1 - ry * Fl0;
             }
         }
+#endif
         Fx += Fl0;
         Fyz += f2{Fl1, Fl2};
         Mx += Ml0;
         My += Ml1;
         Mz += Ml2;
+#ifdef HG_ISA_MARK
+        asm volatile("; GEAR_END");
+#endif
     }
 
     // ---- equations of motion (:448-470)

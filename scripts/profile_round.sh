@@ -9,14 +9,23 @@ DT=${DT:-0.01}
 D=gpurun_out/prof_$TAG
 mkdir -p $D
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o bench -- python3 bench.py --envs $N --dt $DT --task ${TASK:-hover} --steps 1000 --repeats 2 --no-secondary --no-cpu-baseline --no-parity > $D/trace.log 2>&1 || { echo "trace failed"; tail -20 $D/trace.log; exit 3; }
+# ageing: the trace runs the bench's default (60 simulated s); the counter passes, where every dispatch
+# is collected separately, age ${PMC_AGE:-20} s (the population is mixed after about 10 s, the
+# time-limit cohort aside)
+echo "[$TAG] trace"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o bench -- python3 bench.py --envs $N --dt $DT --task ${TASK:-hover} --steps ${TRACE_STEPS:-1000} --repeats 2 --no-secondary --no-cpu-baseline --no-parity > $D/trace.log 2>&1 || { echo "trace failed"; tail -20 $D/trace.log; exit 3; }
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS" \
            "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE" \
            "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set --output-format csv -d $D/pmc$i -o run -- python3 bench.py --envs $N --dt $DT --task ${TASK:-hover} --steps 200 --warmup 20 --repeats 1 --no-secondary --no-cpu-baseline --no-parity > $D/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $D/pmc$i.log; exit 4; }
+  echo "[$TAG] pmc pass $i: $set"
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set --output-format csv -d $D/pmc$i -o run -- python3 bench.py --envs $N --dt $DT --task ${TASK:-hover} --steps 200 --warmup 20 --repeats 1 --age-seconds ${PMC_AGE:-20} --no-secondary --no-cpu-baseline --no-parity > $D/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $D/pmc$i.log; exit 4; }
 done
-python3 scripts/summarize_prof.py $D $TAG $N $DT ${TASK:-hover}
+python3 scripts/summarize_prof.py $D $TAG $N $DT ${TASK:-hover} > $D/summary.txt
+# profiles/ does not travel back from the box, and the raw traces exceed gpurun_out's 64 MiB: keep the
+# summaries, drop the per-dispatch CSVs
+mkdir -p gpurun_out/sum_$TAG && cp profiles/${TAG}_* gpurun_out/sum_$TAG/ && find $D -name "*.csv" ! -name "*kernel_stats.csv" -delete
+echo "[$TAG] done"
 # profiles/ does not travel back from the box: rerun the summariser locally on gpurun_out/prof_$TAG
