@@ -10,6 +10,7 @@ run --envs 262144 --dt 0.01 --task forward_flight
 run --envs 1048576 --dt 0.01 --steps 500
 run --envs 4194304 --dt 0.01 --steps 200 --no-parity
 run --envs 65536 --dt 0.01 --reset-mode retrim --steps 500 --no-parity
+run --envs 65536 --dt 0.01 --reset-mode retrim --autoreset-mode next_step --steps 500 --no-parity
 run --envs 262144 --dt 0.01 --task forward_flight --reset-mode retrim --steps 300 --no-parity
 python - <<'PY'
 import json
