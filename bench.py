@@ -807,7 +807,7 @@ def main():
                     "note": "step_async(with_reset_info=True): reset_index + final_obs compaction "
                             "(hg_step_chained; a memset node per captured step), hipGraph"}
                 # HeliVecEnv.step() as an RL loop calls it: eager, lazy info
-                Ke = min(K, 200)
+                Ke = 200   # (its own window length: 20 eager launches would carry the HIP events' latency)
 
                 def eager_api():
                     for k in range(Ke):

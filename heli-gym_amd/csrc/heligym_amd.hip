@@ -664,7 +664,7 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
 // deferred resets store only their step counter while those trims write the rest.  Both parts fit
 // two waves per SIMD (<= 256 VGPRs), so at one step wave per SIMD a trim wave shares a SIMD with a
 // step wave; the trims, dispatched first, are the long pole.  One queue and no cross-stream events:
-// dependent work on another queue waits about 10 us per hop on MI355X (profiles/r04_ov_trace.txt).
+// dependent work on another queue waited about 10 us per hop on MI355X (scripts/r04_ov_trace.py).
 template <int TASK, bool BAKED>
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2))) void step_ov_kernel(
     float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p, ParamArg Pa,
