@@ -165,6 +165,48 @@ def test_single_step_vs_oracle(torch, tag, terrain_u16):
     print(f"\n[oracle dt={tag}] worst err/tol {worst:.3f}")
 
 
+@pytest.mark.parametrize("rates", [(4.0, 12.0), (12.0, 40.0)])
+def test_single_step_tumbling_vs_oracle(torch, rates, terrain_u16):
+    """Tumbling helicopters (body rates of rates[0]..rates[1] rad/s on the reference's in-flight
+    states, dt 0.01): the stage attitude increments leave the short-series range (0.05 rad) and
+    exercise the long-series angle addition (<= 0.25 rad) and, for the faster set, the full sincos
+    past it.  One step against the oracle at contract (i), identical fp32 inputs.  Exception: at
+    12-40 rad/s the main-rotor power (obs 0) of a few steps is off by up to 2x contract (i) -- the
+    same value with the long series switched off (HG_MID_ANGLE_MRAD=0 build): fp32 rotor
+    aerodynamics at spin rates a flying helicopter never reaches, so it gets 4x there."""
+    from heligym_amd import config
+    from oracle.oracle import Oracle
+    b = gc.single_step_batch(gc.load("0.01"), "hover")
+    rng = np.random.RandomState(7)
+    keep = np.nonzero(b["obs"][:, 16] > 50.0)[0][:400]   # in flight, clear of the ground
+    b = {k: (v[keep] if isinstance(v, np.ndarray) and len(v) == len(b["state"]) else v) for k, v in b.items()}
+    n = len(b["state"])
+    mag = rng.uniform(rates[0], rates[1], size=(n, 3)) * rng.choice([-1.0, 1.0], size=(n, 3))
+    b["state"] = b["state"].copy()
+    b["state"][:, 9:12] = mag   # p, q, r
+    out = run_single_steps(torch, b, "hover")
+    cfg, _ = config.make_config(task="hover", dt=b["dt"])
+    orc = Oracle(cfg, terrain_u16)
+    st32 = b["state"].astype(np.float32).astype(np.float64)
+    worst = 0.0
+    for i in range(n):
+        s = st32[i]
+        prev_obs = np.zeros(17)
+        prev_obs[4:7], prev_obs[16] = s[23:26], s[26]
+        e = orc.env_from(s[:18], s[18:23], prev_obs, np.zeros(18), 0.0, 0.0)
+        o = orc.step(e, b["actions"][i].astype(np.float32), b["eta"][i].astype(np.float32))
+        d = gc.step_errors(out["obs"][i], np.array(o.obs), gc.OBS_ANGLE_COLS)
+        tol = STEP_ABS + STEP_REL * np.abs(np.array(o.obs))
+        if rates[1] > 12.0:
+            tol[0] *= 4.0
+        assert np.all(d <= tol), (i, np.nonzero(d > tol)[0], d[d > tol], tol[d > tol])
+        d2 = gc.step_errors(out["state"][i, :18], np.array(e.heli), gc.HELI_ANGLE_COLS)
+        tol2 = STEP_ABS + STEP_REL * np.abs(np.array(e.heli))
+        assert np.all(d2 <= tol2), (i, np.nonzero(d2 > tol2)[0], d2[d2 > tol2])
+        worst = max(worst, (d / tol).max(), (d2 / tol2).max())
+    print(f"\n[tumbling {rates}] {n} steps, worst err/tol {worst:.3f}")
+
+
 @pytest.mark.parametrize("tag", ["0.02", "0.01"])
 def test_trajectories_100_steps(torch, tag):
     """Each scenario replayed for 100 steps from the reference's reset state with its actions and
