@@ -464,7 +464,30 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
 #endif
         const float zh = c.g.zh(z);
         const f2 B22 = B12;
-#if HG_GEAR_FACTORED
+#if HG_GEAR_FACTORED == 2
+        // Force and contact velocity per point as the reference forms them (the force bitwise the
+        // per-point form); only the QUIRK moment factored: sum_i r_i x F_acc(i), F_acc(i) = S_i b with
+        // S_i the running sum of the fz, is (sum_i S_i r_i) x b.
+        float Fl0 = 0.f, Fl1 = 0.f, Fl2 = 0.f;
+        float S = 0.f, Rx = 0.f, Ry = 0.f, Rz = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi) {
+            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
+            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
+            if (-pzh - P.wl_cg_ft < 0.f) {
+                const float cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
+                const float vel_z = n2 + (-s1 * cx + B22.x * cy + B22.y * cz);
+                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
+                Fl0 += -s1 * fz; Fl1 += B22.x * fz; Fl2 += B22.y * fz;
+                S = gi == 0 ? fz : S + fz;
+                Rx = rx != 0.f ? (gi == 0 ? S * rx : fmaf(S, rx, Rx)) : Rx;
+                Ry = ry != 0.f ? (gi == 0 ? S * ry : fmaf(S, ry, Ry)) : Ry;
+                Rz = rz != 0.f ? (gi == 0 ? S * rz : fmaf(S, rz, Rz)) : Rz;
+            }
+        }
+        const float bx = -s1, by = B22.x, bz = B22.y;
+        const float Ml0 = Ry * bz - Rz * by, Ml1 = Rz * bx - Rx * bz, Ml2 = Rx * by - Ry * bx;
+#elif HG_GEAR_FACTORED
         // Factored: every contact force is fz_i b with b = (-s1, B22) the third DCM column, so the
         // accumulated force after point i is S_i b (S_i the running sum of the fz), the QUIRK moment
         // sum_i r_i x (S_i b) = (sum_i S_i r_i) x b, and the contact velocity n2 + b.(omega x r_i) =
