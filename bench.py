@@ -666,8 +666,9 @@ def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev
         def rep5():
             for k in range(K5):
                 step5(k)
+        mode_n5 = f"{K5} eager launches (dry run)"
     else:
-        rep5, _k5, _m5 = windows(torch, dev, step5, K5, B, env5)
+        rep5, _k5, mode_n5 = windows(torch, dev, step5, K5, B, env5)
     s_n5, _, _, rs_n5 = timer.run_counted(env5, rep5, R)
     ranks_n5 = timer.per_rank
     return {"workload": f"HeliHover-v0 x {CONFIG5_TOTAL} envs sharded over {world} ranks ({n5} on rank {rank})",
@@ -678,7 +679,7 @@ def config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev
             "without_gather": {"value": CONFIG5_TOTAL * K5 / s_n5, "unit": "env-steps/s",
                                "ms_per_step": s_n5 / K5 * 1e3,
                                "per_rank_ms_per_step": [x / K5 * 1e3 for x in ranks_n5],
-                               "resets_in_window": rs_n5, "mode": f"hipGraphs of {B} steps"},
+                               "resets_in_window": rs_n5, "mode": mode_n5},
             "gather_bytes_per_step_to_rank0": (world - 1) * n5 * 17 * 4, "steps": K5}
 
 
