@@ -18,7 +18,24 @@ namespace hg {
 // math helpers: one overload per precision.  fp32 device versions use the hardware
 // transcendental units (v_log_f32 / v_exp_f32 / v_sqrt_f32).
 HD float m_sqrt(float x) { return sqrtf(x); }
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(HG_SQRT_LIBM)
+// fp64 on the device (the re-trim kernels): v_rsq_f64 and a Goldschmidt iteration with a final fused
+// correction (within an ulp of the correctly rounded root for the model's positive normal
+// arguments), instead of the library sqrt's scaling for denormals and its special-case selects;
+// 0 -> 0 and a negative or NaN argument -> NaN, as the library's.
+HD double m_sqrt(double x) {
+    const double r = __builtin_amdgcn_rsq(x);
+    double g = x * r, h = 0.5 * r;
+    const double e = fma(-g, h, 0.5);
+    g = fma(g, e, g);
+    h = fma(h, e, h);
+    const double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return x == 0.0 ? x : g;
+}
+#else
 HD double m_sqrt(double x) { return sqrt(x); }
+#endif
 HD float m_fabs(float x) { return fabsf(x); }
 HD double m_fabs(double x) { return fabs(x); }
 HD float m_floor(float x) { return floorf(x); }

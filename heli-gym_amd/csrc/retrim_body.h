@@ -417,22 +417,28 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             const hg::Params<double>& P = opaque_const<ConstP>(a.P);
             const hg::TrimSetup& T = opaque_const<ConstT>(a.T + (a.setup_stride ? job : 0));
             // ---- one evaluation round (every x - s dir is the same fused operation wherever formed)
+            // every lane forms x - s dir with its own s (a Jacobian lane: the full step of a normal
+            // round, else 0; a trial lane: 2^-j; the fused form with s = 0 is x itself), and a
+            // Jacobian lane adds its +-eps to its own column: the same operations as branching per
+            // lane class, with one select per component instead of three
+            const double sl = l < 32 ? (kind == kRoundNormal ? 1.0 : 0.0)
+                                     : ((kind == kRoundNormal && j < hg::kTrimLineSearch) ? ldexp(1.0, -j) : 0.0);
+            const double pe = l < 16 ? eps : -eps;
             double xe[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                const double base = kind == kRoundNormal ? fma(-1.0, dir[k], x[k]) : x[k];
-                double v;
-                if (l < 32) {
-                    v = k == c ? (l < 16 ? base + eps : base - eps) : base;
-                } else {
-                    const double step = (kind == kRoundNormal && j < hg::kTrimLineSearch) ? ldexp(1.0, -j) : 0.0;
-                    v = fma(-step, dir[k], x[k]);
-                }
-                xe[k] = v;
+                const double b = fma(-sl, dir[k], x[k]);
+                xe[k] = (l < 32 && c == k) ? b + pe : b;
             }
             RSTAMP(1 + 4 * round, "v"(xe[0]));
             if (kind != kRoundJacobian || l < 32) {
+#ifdef HG_ISA_MARK
+                asm volatile("; EVAL_BEGIN");
+#endif
                 trim_eval(P, T, xe, W, ye, ext);
+#ifdef HG_ISA_MARK
+                asm volatile("; EVAL_END");
+#endif
                 double t = 0.0;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) t = fma(ye[k] - T.yt[k], ye[k] - T.yt[k], t);
