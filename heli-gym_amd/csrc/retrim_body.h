@@ -353,8 +353,8 @@ __device__ unsigned g_rt_dbg_n;
 __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, int64_t stride) {
     // the +-eps evaluations E[j][k] of the current Newton step, row j (the evaluating lane) at a stride
     // of kEStride doubles: lane j's 16 writes of a 16-double stride all hit the same two banks
-    __shared__ double sE[32 * kEStride];
-    __shared__ double sR[16];        // its right-hand side y - y*
+    __shared__ double sE[42 * kEStride];   // rows 32..41: the line-search trials' evaluations
+    __shared__ double sYt[16];       // the trim's target derivatives y* (its right-hand side is y(src) - y*)
     __shared__ double sX[16];        // the solution (Newton direction), by column
     __shared__ double sExt[7];       // observation terms of the current iterate
     __shared__ double sRow[HG_GJ_LDS ? 64 * kRowStride : 2];   // HG_GJ_LDS: the rows of the solve
@@ -390,6 +390,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             continue;
         }
         const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];
+        if (l < 16) sYt[l] = T.yt[l];   // (read after the first round's lds_order)
         double W[3] = {P.wm[0], P.wm[1], P.wm[2]};   // NULL wind: the mean wind (helicopter.py:55)
         if (a.recs) {
             W[0] = (double)__int_as_float(rec.y);
@@ -445,6 +446,9 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                 te = t;
             }
             RSTAMP(2 + 4 * round, "v"(te));
+#ifdef HG_ISA_MARK
+            asm volatile("; ACC_BEGIN");
+#endif
             if (kind != kRoundJacobian) {
                 // ---- accept a trial (or take the base point)
                 bool have_jac = true;
@@ -474,15 +478,14 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             // ---- Newton direction: the evaluations and the residual (lane src holds y) into LDS,
             // then the solve, one row per lane
             lds_order();   // the previous solve's reads are done
-            if (l < 32) {
+            if (l < 42) {   // the Jacobian lanes and the trials: the residual is row src's y - y*
 #pragma unroll
                 for (int k = 0; k < 16; ++k) sE[l * kEStride + k] = ye[k];
             }
-            if (l == src) {
-#pragma unroll
-                for (int k = 0; k < 16; ++k) sR[k] = ye[k] - T.yt[k];
-            }
             lds_order();
+#ifdef HG_ISA_MARK
+            asm volatile("; ACC_END");
+#endif
             RSTAMP(3 + 4 * round, "v"(ye[0]));
 #if HG_GJ_SPLIT
             {
@@ -493,7 +496,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                     A4[jj] = sE[(4 * jj + q) * kEStride + i];
                     Em4[jj] = sE[(4 * jj + q + 16) * kEStride + i];
                 }
-                double b = sR[i];
+                double b = sE[src * kEStride + i] - sYt[i];
 #pragma unroll
                 for (int jj = 0; jj < 4; ++jj) A4[jj] = (A4[jj] - Em4[jj]) * (0.5 / eps);
                 uint32_t live = 0xFFFFFFFFu;
@@ -525,7 +528,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                     A[q] = sE[q * kEStride + i];
                     Em[q] = sE[(q + 16) * kEStride + i];
                 }
-                double b = sR[i];
+                double b = sE[src * kEStride + i] - sYt[i];
 #pragma unroll
                 for (int q = 0; q < 16; ++q) A[q] = (A[q] - Em[q]) * (0.5 / eps);
                 uint32_t live = 0xFFFFFFFFu;   // the key mask of a row not yet used as a pivot
