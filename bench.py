@@ -815,8 +815,14 @@ def main():
                         env.step(bank[k % B])
                 eager_api()
                 s_api, s_api_all, _, rs_api = timer.run_counted(env, eager_api, 5)   # median of 5 windows (host jitter)
+                # the same step() calls graph-replayed: what the eager launches cost beyond the
+                # step's own work (step() also writes its auto-resets' terminal observations)
+                rep_sg, _k4, _m = windows(torch, dev, lambda k: env.step(bank[k % B]), Ke, B, env)
+                s_sg, _, _, _ = timer.run_counted(env, rep_sg, 3)
+                del _k4
                 secondary["step_api_eager"] = {
                     "value": total_envs * Ke / s_api, "unit": "env-steps/s", "ms_per_step": s_api / Ke * 1e3,
+                    "graph_replayed_ms_per_step": s_sg / Ke * 1e3,
                     "steps": Ke, "windows_s": s_api_all, "resets_in_window": rs_api,
                     "note": "HeliVecEnv.step() as an RL loop calls it: eager launch of the plain "
                                          "kernel (hg_step_rows: reset envs flagged in the info bytes, their "

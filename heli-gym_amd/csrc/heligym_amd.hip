@@ -515,9 +515,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     // uncompacted reset info (hg_step_rows): the terminal observation at the env's own row, in a
     // wave-uniform branch taken only by waves with a reset
     if (!MULTI && a.final_obs_rows && __ballot(do_reset)) {
-        if (do_reset) {
+        if (do_reset) {   // the 68-byte row as four 16-byte stores and one dword (dword-aligned rows)
+            typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+            f4u* row = reinterpret_cast<f4u*>(a.final_obs_rows + i * 17);
 #pragma unroll
-            for (int c = 0; c < 17; ++c) a.final_obs_rows[i * 17 + c] = obs[c];
+            for (int q = 0; q < 4; ++q) row[q] = f4u{obs[4 * q], obs[4 * q + 1], obs[4 * q + 2], obs[4 * q + 3]};
+            a.final_obs_rows[i * 17 + 16] = obs[16];
         }
     }
 
