@@ -348,11 +348,13 @@ namespace {
 // compile-time, so the hot kernel has no data-independent branches to merge around.
 // The body is a device function so that the run-time specialised code objects (step_rtc.hip) wrap
 // the same code in kernels of their own names.
-template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool NTS>
+template <int TASK, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool NTS, int HELP = 0>
 __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p,
                                           ParamArg Pa, const Template<float>* __restrict__ Tp, const StepArgs& a,
                                           int64_t bid) {
-    __shared__ float s_obs[kStepBlock * HG_N_OBS];   // one 64-row slice per wave
+    static_assert(HELP == 0 || (!ETA && !MULTI), "wind helper waves: in-kernel noise, one step per launch");
+    __shared__ float s_obs[(HELP ? HELP * 64 : kStepBlock) * HG_N_OBS];   // one 64-row slice per wave
+    __shared__ float s_wind[HELP ? HELP * 8 * 64 : 1];   // HELP: each tile's wind output and wind state
     constexpr bool kNTS = NT || NTS;   // non-temporal output stores
     const Params<float>& P0 = *Pa;   // model constants: scalar loads from a device copy
     // BAKED: the default airframe's constants as instruction literals (baked.h); only the runtime
@@ -360,8 +362,11 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     Params<float> PB;
     if constexpr (BAKED) PB = hg::bake(*Pa);
     const int lane = threadIdx.x & 63;
-    const int wv = kStepBlock == 64 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform
-    const int64_t tile = bid * (kStepBlock / 64) + wv;
+    // HELP: blocks of HELP tiles, waves 0 .. HELP-1 step them, waves HELP .. 2 HELP-1 run their noise and
+    // wind step (helper wave j + HELP for tile j) and hand it over in LDS
+    const int wave_id = (kStepBlock == 64 && HELP == 0) ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wv = HELP ? wave_id % (HELP ? HELP : 1) : wave_id;   // uniform
+    const int64_t tile = bid * (HELP ? HELP : kStepBlock / 64) + wv;
     const int64_t blk0 = tile * 64;   // this wave's first env
     const int tid = lane;
     const int64_t i = blk0 + tid;
@@ -383,6 +388,29 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
         g_timing[i >> 6][16] = 0;
     }
 #endif
+    if constexpr (HELP > 0) {
+        const bool helper = wave_id >= HELP;
+        if (tile * 64 >= n_p) {   // (a last block's missing tiles: both waves meet at the barrier)
+            asm volatile("s_barrier" ::: "memory");
+            return;
+        }
+        if (helper) {   // the tile's noise and wind step (Heli.step :195-199), the same code as below
+            const Params<float>& PH = BAKED ? PB : P0;
+            const f32x4 g0 = ld_lane(GRP(st_b, 0), lt), g1 = ld_lane(GRP(st_b, 1), lt), g2 = ld_lane(GRP(st_b, 2), lt),
+                        g3 = ld_lane(GRP(st_b, 3), lt);
+            float ws[5], carry[4], eta[3], W[3];
+            carry[3] = g1.z; carry[0] = g1.w; carry[1] = g2.x; carry[2] = g2.y;
+            ws[0] = g2.z; ws[1] = g2.w; ws[2] = g3.x; ws[3] = g3.y; ws[4] = g3.z;
+            draw_eta<false>(a, seed_p, envoff_p, PH, 0, blk0, lo, __float_as_int(g0.w), __float_as_int(g1.x), eta);
+            hg::wind_step_f32(PH, ws, carry, eta, W);
+            float* sw = s_wind + wv * 8 * 64 + lane;
+            sw[0] = W[0]; sw[64] = W[1]; sw[128] = W[2];
+#pragma unroll
+            for (int c = 0; c < 5; ++c) sw[(3 + c) * 64] = ws[c];
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            return;
+        }
+    }
     TSTAMP(0, "v"(tid));
     // reset template (heli[18] | carry[4] | obs[17]) one float per lane, requested with the state so
     // that a reset costs no round trip at the end (and no late load is outstanding when the step
@@ -424,22 +452,38 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     const hg::GroundTexels tex_c = hg::ground_fetch(a.hmap, cell_c);
 
     TSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(epi), "v"(carry[3]), "v"(ws[4]));
+    float W[3];
+    hg::StepCtx ctx;
+    hg::Att2 a0;
+    if constexpr (HELP > 0) {
+        // the wind-independent part of the step's shared context while the helper wave runs the wind
+        const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
+        ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, 0.f, 0.f, 0.f, h_c, hs[17]);
+        a0 = hg::att0(hs);
+        asm volatile("s_barrier" ::: "memory");
+        const float* sw = s_wind + wv * 8 * 64 + lane;
+        W[0] = sw[0]; W[1] = sw[64]; W[2] = sw[128];
+#pragma unroll
+        for (int c = 0; c < 5; ++c) ws[c] = sw[(3 + c) * 64];
+        ctx.W0 = W[0]; ctx.W1 = W[1]; ctx.W2 = W[2];
+    } else {
     // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
     float eta[3];
     draw_eta<ETA>(a, seed_p, envoff_p, P, so, blk0, lo, step, epi, eta);
 
     // ground height under the committed position (F6), wind step (Heli.step :195-199)
     TSTAMP(2, "v"(eta[2]), "v"(eta[0]));
-    float W[3];
     hg::wind_step_f32(P, ws, carry, eta, W);
     TSTAMP(3, "v"(W[2]), "v"(W[0]));
     const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
 
     TSTAMP(4, "v"(h_c.delta), "v"(h_c.hi));
+    ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, W[0], W[1], W[2], h_c, hs[17]);
+    a0 = hg::att0(hs);
+    }
     // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
-    const hg::StepCtx ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, W[0], W[1], W[2], h_c, hs[17]);
     float k[18], obs[17];
-    hg::rk4_step_f32<NT>(P, ctx, hs, k, obs);   // NT: the launch is one wave per SIMD
+    hg::rk4_step_f32<NT>(P, ctx, hs, k, obs, a0);   // NT: the launch is one wave per SIMD
 #if HG_EARLY_POST
     // the terrain texels under the post-step position (the flags' ground height), requested now so
     // that their latency hides behind the wraps and the reward
@@ -660,6 +704,29 @@ __global__ __launch_bounds__(kStepBlock, NT ? HG_MIN_WAVES : HG_MIN_WAVES_BULK) 
                                                       const Template<float>* __restrict__ Tp, const StepArgs a) {
     step_body<TASK, ETA, NT, FEAT, MULTI, BAKED, NTS>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a, blockIdx.x);
 }
+
+// Small batches (up to half a wave per SIMD): each block is a tile's wave and a helper wave that runs
+// the tile's noise and wind step (no input from the helicopter state) while the tile's wave loads
+// its state and forms the rest of the step's context (density, controls, terrain, attitude
+// sin/cos), the wind handed over in LDS at one barrier.  Bitwise the one-wave kernel (tested).
+// Per step, against the one-wave kernel: 4 096 envs 5.80 -> 5.63 us, 16 384 6.29 -> 6.08,
+// 32 768 6.73 -> 6.63 (profiles/r04_helper_ab.txt).  Not used at a wave per SIMD, where the helpers
+// share SIMDs with the stepping waves: 65 536 envs 7.39 -> 7.44 us (blocks of 2 or 4 tiles with their
+// helpers: 8.81, 7.59).
+#ifndef HG_HELPER   // tiles per block in the small-batch helper kernel; 0: none
+#define HG_HELPER 1
+#endif
+#ifndef HG_HELPER_DIV   // the helper kernel up to resident_envs / HG_HELPER_DIV envs (2: two tiles per CU)
+#define HG_HELPER_DIV 2
+#endif
+#if HG_HELPER > 0
+template <int TASK, bool FEAT, bool BAKED>
+__global__ __launch_bounds__(128 * HG_HELPER, 1) void step_help_kernel(float* __restrict__ state_p, int64_t n_p, uint64_t seed_p,
+                                                                    int64_t envoff_p, ParamArg Pa,
+                                                                    const Template<float>* __restrict__ Tp, const StepArgs a) {
+    step_body<TASK, false, true, FEAT, false, BAKED, false, HG_HELPER>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a, blockIdx.x);
+}
+#endif
 
 #ifndef HG_RTC
 // reset_mode RETRIM with next-step auto-reset (hg_env::ov): one launch holds the trims of the previous
@@ -1309,6 +1376,14 @@ static inline unsigned retrim_grid(int64_t jobs) {
 // 28-word tile three are (4 M: 254.6 against 257.8 us, interleaved A/B), so the cap is gone.
 template <int T, bool ETA, bool NT, bool FEAT, bool MULTI, bool BAKED, bool NTS = false>
 static void launch_step(const hg_env* e, hipStream_t s, const StepArgs& a) {
+#if HG_HELPER > 0
+    if constexpr (NT && !ETA && !MULTI) if (e->n <= e->resident_envs / HG_HELPER_DIV) {
+        const unsigned tiles = (unsigned)((e->n + 63) / 64);
+        hipLaunchKernelGGL((step_help_kernel<T, FEAT, BAKED>), dim3((tiles + HG_HELPER - 1) / HG_HELPER),
+                           dim3(128 * HG_HELPER), 0, s, STEP_KARGS(e), a);
+        return;
+    }
+#endif
     const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock);
     hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED, NTS>), dim3(grid), dim3(kStepBlock), 0, s,
                        STEP_KARGS(e), a);

@@ -618,14 +618,19 @@ HD void from_x16(const X16& x, float* s) {   // (s[2], s[3], the rotor azimuths,
 
 // One RK4 step of the 18-state model (dynamics.py:158-171): hs advanced in place, k4 (the
 // reference's state_dots, what the reward reads) in d, the stage-4 observation in obs.
+// (sin, cos) of the committed attitude (phi, theta, psi = hs[12], hs[13], hs[14])
+HD Att2 att0(const float* hs) {
+    Att2 a0;
+    a0.a[0] = sincos2(hs[12]);
+    a0.a[1] = sincos2(hs[13]);
+    a0.a[2] = sincos2(hs[14]);
+    return a0;
+}
+
 template <bool LONE>
 HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,
-                     float* __restrict__ obs) {
+                     float* __restrict__ obs, const Att2& a0) {
     X16 h = to_x16(hs);
-    Att2 a0;
-    a0.a[0] = sincos2(h.pp.x);
-    a0.a[1] = sincos2(h.rt.y);
-    a0.a[2] = sincos2(h.pp.y);
     X16 k, acc, st;
 #ifndef HG_PIN_CONSTANTS
 #define HG_PIN_CONSTANTS 1
@@ -647,6 +652,12 @@ HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict
     from_x16(k, d);
     d[2] = P.mr_OMEGA;
     d[3] = P.tr_OMEGA;
+}
+
+template <bool LONE>
+HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,
+                     float* __restrict__ obs) {
+    rk4_step_f32<LONE>(P, c, hs, d, obs, att0(hs));
 }
 
 }  // namespace hg

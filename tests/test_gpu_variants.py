@@ -62,6 +62,27 @@ def test_nt_variant_equals_bulk_variant(torch):
     assert resets > 0
 
 
+def test_small_batch_helper_kernel_equals_lone_wave(torch):
+    """A batch of at most two tiles per CU runs the helper kernel (a second wave per block steps the
+    tile's noise and wind, heligym_amd.hip step_help_kernel); a larger one the one-wave kernel.  The
+    first H envs of a 3 H batch against a batch of H (ragged last tile): every observation, reward
+    and done flag and the final state bitwise equal, resets included."""
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    H = 2 * 64 * cus - 61
+    assert H % 64 and 3 * H > 2 * 64 * cus and 3 * H <= 2 * 64 * 4 * cus
+    full = _run(torch, 3 * H, 0, 300)
+    small = _run(torch, H, 0, 300)
+    resets = 0
+    for f, a in zip(full, small):
+        for j in range(3):
+            if f[j] is None:
+                continue
+            np.testing.assert_array_equal(f[j][:H], a[j])
+        if f[2] is not None:
+            resets += int(f[2][:H].sum())
+    assert resets > 0
+
+
 @pytest.mark.parametrize("variant", ["heavy", "wing"])
 def test_runtime_specialised_kernel_bitwise_equals_generic(torch, variant, tmp_path, monkeypatch):
     """Another airframe (the heavier one with other rotor speeds; the winged one) stepped with its
