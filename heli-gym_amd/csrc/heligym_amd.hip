@@ -422,7 +422,10 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     float hs[18], ws[5], carry[4];
     int32_t step, succ, epi;
     {
-        const f32x4 g0 = ld_lane(GRP(st_b, 0), lt), g1 = ld_lane(GRP(st_b, 1), lt), g2 = ld_lane(GRP(st_b, 2), lt),
+        // (HELP: group 2 -- carry[1..2], wind state -- is the helper wave's; the carry is rewritten
+        // at the end of every step and the wind state comes back from the helper)
+        const f32x4 g0 = ld_lane(GRP(st_b, 0), lt), g1 = ld_lane(GRP(st_b, 1), lt),
+                    g2 = HELP ? f32x4{0.f, 0.f, 0.f, 0.f} : ld_lane(GRP(st_b, 2), lt),
                     g3 = ld_lane(GRP(st_b, 3), lt), g4 = ld_lane(GRP(st_b, 4), lt), g5 = ld_lane(GRP(st_b, 5), lt),
                     g6 = ld_lane(GRP(st_b, 6), lt);
         hs[15] = g0.x; hs[16] = g0.y; hs[17] = g0.z; step = __float_as_int(g0.w);
@@ -454,12 +457,13 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     TSTAMP(1, "v"(hs[17]), "v"(act.w), "v"(epi), "v"(carry[3]), "v"(ws[4]));
     float W[3];
     hg::StepCtx ctx;
-    hg::Att2 a0;
+    hg::RK4Step<NT, (HELP > 0)> rk;   // NT: the launch is one wave per SIMD; HELP: stage 1 split
     if constexpr (HELP > 0) {
-        // the wind-independent part of the step's shared context while the helper wave runs the wind
+        // the wind-independent part of the step's shared context and of stage 1 (kinematics, gear)
+        // while the helper wave runs the wind
         const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
         ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, 0.f, 0.f, 0.f, h_c, hs[17]);
-        a0 = hg::att0(hs);
+        rk.begin(P, ctx, hs, hg::att0(hs));
         asm volatile("s_barrier" ::: "memory");
         const float* sw = s_wind + wv * 8 * 64 + lane;
         W[0] = sw[0]; W[1] = sw[64]; W[2] = sw[128];
@@ -479,11 +483,11 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
 
     TSTAMP(4, "v"(h_c.delta), "v"(h_c.hi));
     ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, W[0], W[1], W[2], h_c, hs[17]);
-    a0 = hg::att0(hs);
+    rk.begin(P, ctx, hs, hg::att0(hs));
     }
     // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
     float k[18], obs[17];
-    hg::rk4_step_f32<NT>(P, ctx, hs, k, obs, a0);   // NT: the launch is one wave per SIMD
+    rk.finish(P, ctx, hs, k, obs);
 #if HG_EARLY_POST
     // the terrain texels under the post-step position (the flags' ground height), requested now so
     // that their latency hides behind the wraps and the reward

@@ -330,11 +330,155 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
     return a;
 }
 
+// Stage parts that do not read the wind: the kinematics and the landing gear (:385-398).  Inlined in
+// place in every stage; the small-batch kernel forms stage 1's (stage_pre) while a helper wave runs
+// the wind step (heligym_amd.hip step_help_kernel).  The same expressions either way.
+struct Kin {
+    f2 sqth, n01;
+    float phid, psid, n2;
+};
+
+HD Kin kinematics(const X16& s, const Att2& at) {
+    // kinematic.py:3-29, :423-431.  Rotations are written so that every sign flip and lane swap is an
+    // operand modifier of the packed instruction: (s, c).yx * (x, -x) etc.
+    const float v = s.uv.y, p = s.pq.x, q = s.pq.y;
+    const f2 SC0 = at.a[0], SC1 = at.a[1], SC2 = at.a[2];
+    const float s1 = SC1.x, c1 = SC1.y;
+    Kin o;
+    const float ic1 = m_rcp(c1);
+    o.sqth = fma_sw_bxn(SC0, s.rt, SC0 * q);                    // SC0 q + SC0.yx (r, -r) = (s0 q + c0 r, theta')
+    o.phid = p + (s1 * ic1) * o.sqth.x;
+    o.psid = ic1 * o.sqth.x;
+    // NED velocity B^T uvw = Rz^T Ry^T Rx^T uvw
+    const f2 yz1 = fma_nbx(SC0, s.wz, SC0.yx * v);              // SC0.yx v + SC0 (-w, w) = Rx^T (y, z)
+    const f2 xz2 = fma_sw_bxn(SC1, s.uv, SC1 * yz1.y);         // SC1.yx (u, -u) + SC1 yz1.y = Ry^T (x, z)
+    o.n01 = fma_nbx(SC2, yz1, SC2.yx * xz2.x);                 // SC2.yx xz2.x - SC2 (y, -y) = Rz^T (x, y)
+    o.n2 = xz2.y;
+    return o;
+}
+
+// The landing gear's loads added into the totals, only where some lane of the wave may touch
+// (`ran`: the wave took the branch).  QUIRK: the moment uses the ACCUMULATED force (:397).
+HD void gear_add(const Params<float>& P, const StepCtx& c, const X16& s, const Att2& at, float n2, float& Fx, f2& Fyz,
+                 float& Mx, float& My, float& Mz, bool& ran) {
+    const float z = s.wz.y, p = s.pq.x, q = s.pq.y, r = s.rt.x;
+    const f2 SC0 = at.a[0];
+    const float s1 = at.a[1].x, c1 = at.a[1].y;
+#if !defined(HG_ISA_HOT) && !defined(HG_ISA_NOGEAR)
+    if (wave_any(z > c.cz)) {
+#else
+    if (false) {
+#endif
+        HG_STAGE_FLAG(2);
+#ifdef HG_ISA_MARK
+        asm volatile("; GEAR_BEGIN");
+#endif
+        const float zh = c.g.zh(z);
+        const f2 B22 = SC0 * c1;   // (B12, B22); B02 = -s1
+#if HG_GEAR_FACTORED == 2
+        // Force and contact velocity per point as the reference forms them (the force bitwise the
+        // per-point form); only the QUIRK moment factored: sum_i r_i x F_acc(i), F_acc(i) = S_i b with
+        // S_i the running sum of the fz, is (sum_i S_i r_i) x b.
+        float Fl0 = 0.f, Fl1 = 0.f, Fl2 = 0.f;
+        float S = 0.f, Rx = 0.f, Ry = 0.f, Rz = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi) {
+            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
+            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
+            if (-pzh - P.wl_cg_ft < 0.f) {
+                const float cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
+                const float vel_z = n2 + (-s1 * cx + B22.x * cy + B22.y * cz);
+                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
+                Fl0 += -s1 * fz; Fl1 += B22.x * fz; Fl2 += B22.y * fz;
+                S = gi == 0 ? fz : S + fz;
+                Rx = rx != 0.f ? (gi == 0 ? S * rx : fmaf(S, rx, Rx)) : Rx;
+                Ry = ry != 0.f ? (gi == 0 ? S * ry : fmaf(S, ry, Ry)) : Ry;
+                Rz = rz != 0.f ? (gi == 0 ? S * rz : fmaf(S, rz, Rz)) : Rz;
+            }
+        }
+        const float bx = -s1, by = B22.x, bz = B22.y;
+        const float Ml0 = Ry * bz - Rz * by, Ml1 = Rz * bx - Rx * bz, Ml2 = Rx * by - Ry * bx;
+#elif HG_GEAR_FACTORED
+        // Factored: every contact force is fz_i b with b = (-s1, B22) the third DCM column, so the
+        // accumulated force after point i is S_i b (S_i the running sum of the fz), the QUIRK moment
+        // sum_i r_i x (S_i b) = (sum_i S_i r_i) x b, and the contact velocity n2 + b.(omega x r_i) =
+        // n2 + r_i.(b x omega).  The same sums in another order: 4 instead of 12 operations per contact
+        // point for the loads, 3 instead of 9 for the velocity.
+        const float bx = -s1, by = B22.x, bz = B22.y;
+        const float ux = by * r - bz * q, uy = bz * p - bx * r, uz = bx * q - by * p;   // b x omega
+        float S = 0.f, Rx = 0.f, Ry = 0.f, Rz = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi) {
+            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
+            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
+            if (-pzh - P.wl_cg_ft < 0.f) {
+                float ru = rx != 0.f ? rx * ux : 0.f;   // r . (b x omega)
+                ru = ry != 0.f ? fmaf(ry, uy, ru) : ru;
+                ru = rz != 0.f ? fmaf(rz, uz, ru) : ru;
+                const float vel_z = n2 + ru;
+                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
+                // (the first point starts the sums; a zero coordinate of a compiled-in gear point drops
+                // its term, here and above)
+                S = gi == 0 ? fz : S + fz;
+                Rx = rx != 0.f ? (gi == 0 ? S * rx : fmaf(S, rx, Rx)) : Rx;
+                Ry = ry != 0.f ? (gi == 0 ? S * ry : fmaf(S, ry, Ry)) : Ry;
+                Rz = rz != 0.f ? (gi == 0 ? S * rz : fmaf(S, rz, Rz)) : Rz;
+            }
+        }
+        const float Fl0 = S * bx, Fl1 = S * by, Fl2 = S * bz;
+        const float Ml0 = Ry * bz - Rz * by, Ml1 = Rz * bx - Rx * bz, Ml2 = Rx * by - Ry * bx;
+#else
+        float Fl0 = 0.f, Fl1 = 0.f, Fl2 = 0.f, Ml0 = 0.f, Ml1 = 0.f, Ml2 = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi) {
+            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
+            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
+            if (-pzh - P.wl_cg_ft < 0.f) {
+                const float cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
+                const float vel_z = n2 + (-s1 * cx + B22.x * cy + B22.y * cz);
+                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
+                Fl0 += -s1 * fz; Fl1 += B22.x * fz; Fl2 += B22.y * fz;
+                Ml0 += ry * Fl2 - rz * Fl1;
+                Ml1 += rz * Fl0 - rx * Fl2;
+                Ml2 += rx * Fl1 - ry * Fl0;
+            }
+        }
+#endif
+        Fx += Fl0;
+        Fyz += f2{Fl1, Fl2};
+        Mx += Ml0;
+        My += Ml1;
+        Mz += Ml2;
+        ran = true;
+#ifdef HG_ISA_MARK
+        asm volatile("; GEAR_END");
+#endif
+    }
+}
+
+// Stage 1's wind-independent part, formed ahead (the small-batch kernel)
+struct StagePre {
+    Kin kin;
+    bool gear;
+    float Fl0, Ml0, Ml1, Ml2;
+    f2 Fl12;
+};
+
+HD StagePre stage_pre(const Params<float>& P, const StepCtx& c, const X16& s, const Att2& at) {
+    StagePre o;
+    o.kin = kinematics(s, at);
+    o.gear = false;
+    // (-0 + x == x for every x, so the totals later add exactly what the inline form adds)
+    o.Fl0 = -0.f; o.Fl12 = f2{-0.f, -0.f}; o.Ml0 = -0.f; o.Ml1 = -0.f; o.Ml2 = -0.f;
+    gear_add(P, c, s, at, o.kin.n2, o.Fl0, o.Fl12, o.Ml0, o.Ml1, o.Ml2, o.gear);
+    return o;
+}
+
 // One evaluation of the model at stage state s (helicopter_dynamics.py:400-489) -> derivatives k;
 // with OBS also the 17 observations (:471-488) and the total power.
-template <bool OBS>
+template <bool OBS, bool PRE = false>
 HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, const X16& s, const Att2& at, X16& k,
-                  float* __restrict__ obs) {
+                  float* __restrict__ obs, const StagePre* pre = nullptr) {
 #ifdef HG_ISA_MARKS
     asm volatile("; HGMARK stage begin");
 #endif
@@ -342,16 +486,13 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
     const f2 SC0 = at.a[0], SC1 = at.a[1], SC2 = at.a[2];
     const float s0 = SC0.x, c0 = SC0.y, s1 = SC1.x, c1 = SC1.y, s2 = SC2.x, c2 = SC2.y;
 
-    // ---- kinematics (kinematic.py:3-29, :423-431).  Rotations are written so that every sign
-    // flip and lane swap is an operand modifier of the packed instruction: (s, c).yx * (x, -x) etc.
-    const float ic1 = m_rcp(c1);
-    const f2 sqth = fma_sw_bxn(SC0, s.rt, SC0 * q);           // SC0 q + SC0.yx (r, -r) = (s0 q + c0 r, theta')
-    const float phid = p + (s1 * ic1) * sqth.x, psid = ic1 * sqth.x;
-    // NED velocity B^T uvw = Rz^T Ry^T Rx^T uvw
-    const f2 yz1 = fma_nbx(SC0, s.wz, SC0.yx * v);              // SC0.yx v + SC0 (-w, w) = Rx^T (y, z)
-    const f2 xz2 = fma_sw_bxn(SC1, s.uv, SC1 * yz1.y);         // SC1.yx (u, -u) + SC1 yz1.y = Ry^T (x, z)
-    const f2 n01 = fma_nbx(SC2, yz1, SC2.yx * xz2.x);          // SC2.yx xz2.x - SC2 (y, -y) = Rz^T (x, y)
-    const float n2 = xz2.y;
+    (void)s0; (void)c0; (void)s2; (void)c2;
+    // ---- kinematics (kinematic.py:3-29, :423-431)
+    const Kin kin = PRE ? pre->kin : kinematics(s, at);
+    const f2 sqth = kin.sqth;
+    const float phid = kin.phid, psid = kin.psid;
+    const f2 n01 = kin.n01;
+    const float n2 = kin.n2;
     // air-relative body velocity uvw - B W, B = Rx Ry Rz
     const f2 ab = SC2.yx * f2{c.W0, -c.W0} + SC2 * c.W1;       // Rz W (x, y)
     const f2 xg = SC1.yx * ab.x + SC1 * f2{-c.W2, c.W2};       // Ry (x, z)
@@ -451,96 +592,18 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
         Fyz.y += Z_WN;
         power += m_fabs(X_WN * ua);
     }
-    // landing gear (:385-398), only where some lane of the wave may touch.  QUIRK: the moment uses
-    // the ACCUMULATED force (:397).
-#if !defined(HG_ISA_HOT) && !defined(HG_ISA_NOGEAR)
-    if (wave_any(z > c.cz)) {
-#else
-    if (false) {
-#endif
-        HG_STAGE_FLAG(2);
-#ifdef HG_ISA_MARK
-        asm volatile("; GEAR_BEGIN");
-#endif
-        const float zh = c.g.zh(z);
-        const f2 B22 = B12;
-#if HG_GEAR_FACTORED == 2
-        // Force and contact velocity per point as the reference forms them (the force bitwise the
-        // per-point form); only the QUIRK moment factored: sum_i r_i x F_acc(i), F_acc(i) = S_i b with
-        // S_i the running sum of the fz, is (sum_i S_i r_i) x b.
-        float Fl0 = 0.f, Fl1 = 0.f, Fl2 = 0.f;
-        float S = 0.f, Rx = 0.f, Ry = 0.f, Rz = 0.f;
-#pragma unroll
-        for (int gi = 0; gi < 3; ++gi) {
-            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
-            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
-            if (-pzh - P.wl_cg_ft < 0.f) {
-                const float cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
-                const float vel_z = n2 + (-s1 * cx + B22.x * cy + B22.y * cz);
-                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
-                Fl0 += -s1 * fz; Fl1 += B22.x * fz; Fl2 += B22.y * fz;
-                S = gi == 0 ? fz : S + fz;
-                Rx = rx != 0.f ? (gi == 0 ? S * rx : fmaf(S, rx, Rx)) : Rx;
-                Ry = ry != 0.f ? (gi == 0 ? S * ry : fmaf(S, ry, Ry)) : Ry;
-                Rz = rz != 0.f ? (gi == 0 ? S * rz : fmaf(S, rz, Rz)) : Rz;
-            }
+    // landing gear (:385-398)
+    if constexpr (PRE) {
+        if (pre->gear) {
+            Fx += pre->Fl0;
+            Fyz += pre->Fl12;
+            Mx += pre->Ml0;
+            My += pre->Ml1;
+            Mz += pre->Ml2;
         }
-        const float bx = -s1, by = B22.x, bz = B22.y;
-        const float Ml0 = Ry * bz - Rz * by, Ml1 = Rz * bx - Rx * bz, Ml2 = Rx * by - Ry * bx;
-#elif HG_GEAR_FACTORED
-        // Factored: every contact force is fz_i b with b = (-s1, B22) the third DCM column, so the
-        // accumulated force after point i is S_i b (S_i the running sum of the fz), the QUIRK moment
-        // sum_i r_i x (S_i b) = (sum_i S_i r_i) x b, and the contact velocity n2 + b.(omega x r_i) =
-        // n2 + r_i.(b x omega).  The same sums in another order: 4 instead of 12 operations per contact
-        // point for the loads, 3 instead of 9 for the velocity.
-        const float bx = -s1, by = B22.x, bz = B22.y;
-        const float ux = by * r - bz * q, uy = bz * p - bx * r, uz = bx * q - by * p;   // b x omega
-        float S = 0.f, Rx = 0.f, Ry = 0.f, Rz = 0.f;
-#pragma unroll
-        for (int gi = 0; gi < 3; ++gi) {
-            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
-            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
-            if (-pzh - P.wl_cg_ft < 0.f) {
-                float ru = rx != 0.f ? rx * ux : 0.f;   // r . (b x omega)
-                ru = ry != 0.f ? fmaf(ry, uy, ru) : ru;
-                ru = rz != 0.f ? fmaf(rz, uz, ru) : ru;
-                const float vel_z = n2 + ru;
-                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
-                // (the first point starts the sums; a zero coordinate of a compiled-in gear point drops
-                // its term, here and above)
-                S = gi == 0 ? fz : S + fz;
-                Rx = rx != 0.f ? (gi == 0 ? S * rx : fmaf(S, rx, Rx)) : Rx;
-                Ry = ry != 0.f ? (gi == 0 ? S * ry : fmaf(S, ry, Ry)) : Ry;
-                Rz = rz != 0.f ? (gi == 0 ? S * rz : fmaf(S, rz, Rz)) : Rz;
-            }
-        }
-        const float Fl0 = S * bx, Fl1 = S * by, Fl2 = S * bz;
-        const float Ml0 = Ry * bz - Rz * by, Ml1 = Rz * bx - Rx * bz, Ml2 = Rx * by - Ry * bx;
-#else
-        float Fl0 = 0.f, Fl1 = 0.f, Fl2 = 0.f, Ml0 = 0.f, Ml1 = 0.f, Ml2 = 0.f;
-#pragma unroll
-        for (int gi = 0; gi < 3; ++gi) {
-            const float rx = P.lg_loc[gi][0], ry = P.lg_loc[gi][1], rz = P.lg_loc[gi][2];
-            const float pzh = zh + (-s1 * rx + B22.x * ry + B22.y * rz);   // pos_z + h
-            if (-pzh - P.wl_cg_ft < 0.f) {
-                const float cx = q * rz - r * ry, cy = r * rx - p * rz, cz = p * ry - q * rx;
-                const float vel_z = n2 + (-s1 * cx + B22.x * cy + B22.y * cz);
-                const float fz = -(P.lg_C * vel_z + P.lg_K * pzh) + (float)kEps;
-                Fl0 += -s1 * fz; Fl1 += B22.x * fz; Fl2 += B22.y * fz;
-                Ml0 += ry * Fl2 - rz * Fl1;
-                Ml1 += rz * Fl0 - rx * Fl2;
-                Ml2 += rx * Fl1 - ry * Fl0;
-            }
-        }
-#endif
-        Fx += Fl0;
-        Fyz += f2{Fl1, Fl2};
-        Mx += Ml0;
-        My += Ml1;
-        Mz += Ml2;
-#ifdef HG_ISA_MARK
-        asm volatile("; GEAR_END");
-#endif
+    } else {
+        bool ran = false;
+        gear_add(P, c, s, at, n2, Fx, Fyz, Mx, My, Mz, ran);
     }
 
     // ---- equations of motion (:448-470)
@@ -627,16 +690,32 @@ HD Att2 att0(const float* hs) {
     return a0;
 }
 
-template <bool LONE>
-HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,
-                     float* __restrict__ obs, const Att2& a0) {
-    X16 h = to_x16(hs);
-    X16 k, acc, st;
 #ifndef HG_PIN_CONSTANTS
 #define HG_PIN_CONSTANTS 1
 #endif
-    const StepK K = step_k<LONE && HG_PIN_CONSTANTS>(P);
-    stage_f32<false>(P, K, c, h, a0, k, obs);
+// One RK4 step in two parts: begin() forms what stage 1 needs that does not read the wind (the
+// small-batch kernel runs it while its helper wave steps the wind), finish() the rest.
+template <bool LONE, bool PRE1 = false>
+struct RK4Step {
+    X16 h;
+    Att2 a0;
+    StepK K;
+    StagePre pre1;
+    HD void begin(const Params<float>& P, const StepCtx& c, const float* hs, const Att2& a) {
+        h = to_x16(hs);
+        a0 = a;
+        K = step_k<LONE && HG_PIN_CONSTANTS>(P);
+        if constexpr (PRE1) pre1 = stage_pre(P, c, h, a0);
+    }
+    HD void finish(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,
+                   float* __restrict__ obs);
+};
+
+template <bool LONE, bool PRE1>
+HD void RK4Step<LONE, PRE1>::finish(const Params<float>& P, const StepCtx& c, float* __restrict__ hs,
+                                   float* __restrict__ d, float* __restrict__ obs) {
+    X16 k, acc, st;
+    stage_f32<false, PRE1>(P, K, c, h, a0, k, obs, &pre1);
     HG_STAGE_STAMP(5, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<true>(h, k, acc, st, P.half_dt);
     stage_f32<false>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
@@ -652,6 +731,14 @@ HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict
     from_x16(k, d);
     d[2] = P.mr_OMEGA;
     d[3] = P.tr_OMEGA;
+}
+
+template <bool LONE>
+HD void rk4_step_f32(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,
+                     float* __restrict__ obs, const Att2& a0) {
+    RK4Step<LONE> rk;
+    rk.begin(P, c, hs, a0);
+    rk.finish(P, c, hs, d, obs);
 }
 
 template <bool LONE>
