@@ -999,7 +999,11 @@ def main():
                    "per_rank_ms_per_step": [x / K * 1e3 for x in per_rank]},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": f"step_kernel<{args.task.upper()}>", "kernel_avg_us": kern_s * 1e6,
+                     "kernel": (f"step_help_kernel<{args.task.upper()}>"   # (heligym_amd.hip launch_step: a helper
+                                # wave per tile up to half a wave per SIMD, HG_HELPER_DIV)
+                                if torch.cuda.is_available() and args.envs <= 2 * 64 * torch.cuda.get_device_properties(0).multi_processor_count
+                                else f"step_kernel<{args.task.upper()}>"),
+                     "kernel_avg_us": kern_s * 1e6,
                      "kernel_avg_source": "the median timed window (GPU clock stamps around its K launches) / K",
                      "bytes_per_env_step": BYTES_PER_ENV_STEP,
                      "impl_bytes_per_env_step": IMPL_BYTES_PER_ENV_STEP,
