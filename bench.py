@@ -71,6 +71,11 @@ def parse():
     ap.add_argument("--gather-obs", action="store_true",
                     help="headline = BASELINE config 5: obs gathered to rank 0 every step (needs N > 1)")
     ap.add_argument("--no-config5", action="store_true", help="N > 1: skip the config-5 secondary figure")
+    ap.add_argument("--config5-timeout", type=float, default=float(os.environ.get("HG_BENCH_CONFIG5_TIMEOUT", 240)),
+                    help="wall-clock limit (s) of the config-5 child run; past it the child is killed and the line "
+                         "carries config5.error")
+    ap.add_argument("--config5-only", action="store_true",
+                    help="(internal) the config-5 child: measure BASELINE config 5 only, print {'config5': ...}")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
@@ -97,6 +102,79 @@ def launch(args):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
     return subprocess.call(cmd)
+
+
+def run_config5_child(args, world):
+    """BASELINE config 5 (1 048 576 envs over the ranks, RCCL gather to rank 0) in a child run of its
+    own, started by rank 0 BEFORE this process touches the GPU or joins the process group (the other
+    ranks wait in the rendezvous), under a wall-clock limit: an RCCL error, a crash or a hang in the
+    child costs only its own block of the line ({"error": ...}), never the headline.  The child is
+    `torch.distributed.run` over the same N GPUs (or, for the one-rank rehearsal, one process), each
+    of its ranks also bounded by a watchdog (os._exit) a little inside the limit."""
+    import signal
+    import tempfile
+    limit = max(10.0, args.config5_timeout)
+    argv = [a for a in sys.argv[1:] if a != "--config5-only"] + ["--config5-only"]
+    me = os.path.abspath(__file__)
+    if world > 1:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", me, *argv]
+    else:
+        cmd = [sys.executable, me, *argv]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+                        "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS", "TORCHELASTIC_USE_AGENT_STORE",
+                        "TORCH_NCCL_ASYNC_ERROR_HANDLING")}
+    if os.environ.get("HG_BENCH_CONFIG5_NO_WATCHDOG") != "1":   # (CPU test of the parent's kill path)
+        env["HG_BENCH_CONFIG5_WATCHDOG"] = str(limit - 5.0)
+    progress(f"config5: child run ({world} ranks, limit {limit:.0f} s)")
+    t0 = time.perf_counter()
+    with tempfile.TemporaryFile(mode="w+") as out, tempfile.TemporaryFile(mode="w+") as err:
+        p = subprocess.Popen(cmd, stdout=out, stderr=err, env=env, cwd=ROOT, start_new_session=True)
+        try:
+            rc = p.wait(timeout=limit)
+        except subprocess.TimeoutExpired:
+            rc = None
+            for sig, grace in ((signal.SIGTERM, 15), (signal.SIGKILL, 15)):   # the launcher stops its workers
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    break
+                try:
+                    p.wait(timeout=grace)
+                    break
+                except subprocess.TimeoutExpired:
+                    continue
+        out.seek(0)
+        err.seek(0)
+        lines = [ln for ln in out.read().splitlines() if ln.startswith("{")]
+        errtext = err.read()
+        # the exceptions the ranks raised (the launcher's own summary fills the tail)
+        raised = [ln.strip() for ln in errtext.splitlines() if "Error:" in ln or "Exception:" in ln][:6]
+        tail = {"raised": raised, "tail": errtext[-1500:]}
+    wall = time.perf_counter() - t0
+    if rc is None:
+        return {"error": f"config-5 child run killed at its {limit:.0f} s limit", "stderr": tail}
+    if rc != 0 or not lines:
+        return {"error": f"config-5 child run failed (exit status {rc})", "stderr": tail}
+    try:
+        c5 = json.loads(lines[-1])["config5"]
+    except (ValueError, KeyError) as exc:
+        return {"error": f"config-5 child run printed no config5 block ({exc!r})", "stderr": tail}
+    c5["child_wall_s"] = wall
+    return c5
+
+
+def config5_watchdog():
+    """Config-5 child ranks: leave at the limit the parent set, whatever the process is doing (a hang
+    in a collective included), so that the child run ends by itself."""
+    import threading
+    lim = os.environ.get("HG_BENCH_CONFIG5_WATCHDOG")
+    if lim:
+        t = threading.Timer(float(lim), lambda: os._exit(124))
+        t.daemon = True
+        t.start()
 
 
 def cpu_share():
@@ -341,7 +419,7 @@ class TimedGraph:
     in steady state: the GPU is already stepping when the first stamp is taken, and the window holds K
     step kernels with their dependent-launch gaps plus the gap after the first stamp (about 1.6 us).
     HIP events around a short window add about 15 us of event and launch latency to it (20 steps:
-    8.4-8.5 us per step against 7.6-7.7 at 1 000 steps, scripts/r04_batch4.sh), which is why they are
+    8.4-8.5 us per step against 7.6-7.7 at 1 000 steps, profiles/r04_inner_events.txt), which is why they are
     not the window's clock here; they still bracket the whole graph (`event_s`, reported beside it).
     `inner_s()` is the K steps' time, `resets()` the episodes begun in them and the W = 8 untimed
     steps right before them (the first count sits W steps before the first stamp)."""
@@ -370,7 +448,7 @@ class TimedGraph:
             st = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
             if lib.hg_clock_stamp(ctypes.c_void_p(self.stamps[j:j + 1].data_ptr()), st) != 0:
                 raise RuntimeError("hg_clock_stamp failed")
-        # layout (A/B, scripts/r04_batch6.sh): 0 the first episode count right before the first stamp;
+        # layout (A/B, profiles/r04_window_ab.txt): 0 the first episode count right before the first stamp;
         # 1 no counts; 2 (default) W = 8 plain steps between that count and the first stamp -- the
         # steps right after the count kernels run slower (20-step windows: 8.11 / 8.01 / 7.96 us);
         # a pre-roll of 1 000 steps instead of 100: 8.17 -> 7.89 us (the GPU's clock and caches settle)
@@ -699,6 +777,20 @@ def main():
     # HG_BENCH_FORCE_DIST=1: a process group (RCCL) even for one rank, so that the config-5 gather
     # loop runs on hardware with one GPU (gather to itself) -- a rehearsal of the API usage only
     forced = os.environ.get("HG_BENCH_FORCE_DIST") == "1" and world == 1 and not args.dry_run
+    from datetime import timedelta
+    if args.config5_only:
+        config5_watchdog()
+        if os.environ.get("HG_BENCH_CONFIG5_INJECT") == "hang":   # (CPU test hook)
+            time.sleep(3600)
+        if os.environ.get("HG_BENCH_CONFIG5_INJECT") == "fail" and rank == world - 1:
+            raise RuntimeError("injected config-5 failure")
+    want5 = (world > 1 or forced) and not args.no_config5 and not args.no_secondary and not args.gather_obs
+    c5_child = None
+    if want5 and not args.config5_only and rank == 0:
+        c5_child = run_config5_child(args, world)   # before this process touches the GPU
+    # the other ranks wait for rank 0 in the rendezvous while its config-5 child runs; past that, a
+    # collective that does not complete errors out instead of hanging the run
+    pg_timeout = timedelta(seconds=120 + (args.config5_timeout + 60 if want5 and not args.config5_only else 0))
     if forced:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
@@ -709,17 +801,17 @@ def main():
         torch.cuda.synchronize = lambda *a, **k: None   # noqa: E731  (no device in a dry run)
         if world > 1:
             backend = "gloo"
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout)
     elif world > 1 or forced:
         # HG_BENCH_BACKEND=gloo: rehearsal of the N>1 path with several ranks on one GPU (RCCL
         # refuses two ranks on one device); timings from such a run are not a measurement
         backend = os.environ.get("HG_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), timeout=pg_timeout)
         else:
             torch.cuda.set_device(local % torch.cuda.device_count())
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout)
         dev = torch.device(f"cuda:{torch.cuda.current_device()}")
     else:
         torch.cuda.set_device(0)
@@ -739,6 +831,19 @@ def main():
     B = max(1, args.graph_steps)
     K = max(1, args.steps)
     R = max(1, args.repeats)
+
+    if args.config5_only:   # the config-5 child's ranks (run_config5_child)
+        from heligym_amd.distributed import shard_bounds
+        off5, n5 = shard_bounds(CONFIG5_TOTAL, rank, world)
+        env5 = make_env(args, torch, n5, off5, dev)
+        bank5 = action_bank(args, torch, env5, n5, dev, B)
+        age(args, torch, env5, bank5, B)
+        c5 = config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world, dev, backend)
+        if rank == 0:
+            print(json.dumps({"config5": c5}), flush=True)
+        env5.close()
+        dist.destroy_process_group()
+        return
 
     secondary = {}
     head_event_s = None
@@ -925,27 +1030,8 @@ def main():
             envx.close()
             del bankx
 
-        if dist_on and not args.no_config5 and not args.no_secondary:
-            # BASELINE config 5: 1 048 576 envs over the ranks, with and without the gather to rank 0.
-            # A failure here must not cost the headline line: the ranks agree that every one of them
-            # set up its shard before any of them enters a collective.
-            from heligym_amd.distributed import shard_bounds
-            off5, n5 = shard_bounds(CONFIG5_TOTAL, rank, world)
-            ok, err5 = 1, None
-            try:
-                env5 = make_env(args, torch, n5, off5, dev)
-                bank5 = action_bank(args, torch, env5, n5, dev, B)
-                age(args, torch, env5, bank5, B)
-            except Exception as e:   # e.g. out of memory on one rank
-                ok, err5 = 0, repr(e)
-            flag = torch.tensor([ok], dtype=torch.int32, device=dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if int(flag.item()) == 0:
-                secondary["config5"] = {"error": err5 or "another rank failed to set up its shard"}
-            else:
-                secondary["config5"] = config5(args, torch, dist, timer, env5, bank5, n5, B, K, R, rank, world,
-                                               dev, backend)
-                env5.close()
+        if c5_child is not None:   # BASELINE config 5, measured by rank 0's child run before the headline
+            secondary["config5"] = c5_child
 
     if rank != 0:
         if dist_on:

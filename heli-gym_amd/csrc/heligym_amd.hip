@@ -739,6 +739,8 @@ __global__ __launch_bounds__(128 * HG_HELPER, 1) void step_help_kernel(float* __
 // two waves per SIMD (<= 256 VGPRs), so at one step wave per SIMD a trim wave shares a SIMD with a
 // step wave; the trims, dispatched first, are the long pole.  One queue and no cross-stream events:
 // dependent work on another queue waited about 10 us per hop on MI355X (scripts/r04_ov_trace.py).
+// retrim_jobs treats threadIdx.x as the lane of a single wave (Jacobian column, trial, LDS rows)
+static_assert(kStepBlock == 64, "step_ov_kernel's trim blocks are one wave");
 template <int TASK, bool BAKED>
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2))) void step_ov_kernel(
     float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p, ParamArg Pa,
@@ -941,6 +943,35 @@ __global__ __launch_bounds__(kBlock) void random_actions_kernel(float* act, int6
     const float w = hi - lo;
     reinterpret_cast<float4*>(act)[i] =
         make_float4(lo + w * u01(r.x), lo + w * u01(r.y), lo + w * u01(r.z), lo + w * u01(r.w));
+}
+
+// hg_debug_eta: the turbulence noise each env's next in-kernel step draws (wind_dynamics.py:49-52), from
+// its counters (episode step, episode index) in the state tile -- the same function (draw_eta<false>)
+// with the same key, so a step with these normals injected is bitwise the in-kernel step.
+__global__ __launch_bounds__(kBlock) void eta_kernel(const float* state, int64_t n, uint64_t seed, int64_t env_offset,
+                                                     const Params<float>* P, float* out) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const int32_t* ctr = reinterpret_cast<const int32_t*>(state);
+    StepArgs a;   // (read only by the injected-noise form)
+    a.eta = nullptr;
+    float eta[3];
+    draw_eta<false>(a, seed, env_offset, *P, 0, i, 0u, ctr[tix(i, kCtrCol0 + 0)], ctr[tix(i, kCtrCol0 + 2)], eta);
+    out[3 * i + 0] = eta[0];
+    out[3 * i + 1] = eta[1];
+    out[3 * i + 2] = eta[2];
+}
+
+// hg_debug_philox: the device Philox4x32-10 on given counters and keys, rows {c0, c1, c2, c3, k0, k1}
+__global__ __launch_bounds__(kBlock) void philox_kernel(const uint32_t* in, uint32_t* out, int64_t count) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= count) return;
+    const uint32_t* r = in + 6 * i;
+    const U4 o = philox(U4{r[0], r[1], r[2], r[3]}, r[4], r[5]);
+    out[4 * i + 0] = o.x;
+    out[4 * i + 1] = o.y;
+    out[4 * i + 2] = o.z;
+    out[4 * i + 3] = o.w;
 }
 
 // ------------------------------------------------------------------------------ host model
@@ -1275,6 +1306,9 @@ struct hg_env {
     bool ever_captured = false;             // a step was captured into a graph: replays the host cannot see may
                                             // leave any ring slot non-zero, so eager steps zero their own slot
     int64_t setup_batch_cap = 0;
+    // launch counts (hg_debug_launches): step calls, steps holding overlapped re-trims, run-time
+    // specialised / helper / lone-wave / bulk kernel launches
+    mutable int64_t n_launch[6] = {0, 0, 0, 0, 0, 0};
 };
 
 // Every entry point that touches device memory runs on the handle's device (the caller's current
@@ -1385,9 +1419,11 @@ static void launch_step(const hg_env* e, hipStream_t s, const StepArgs& a) {
         const unsigned tiles = (unsigned)((e->n + 63) / 64);
         hipLaunchKernelGGL((step_help_kernel<T, FEAT, BAKED>), dim3((tiles + HG_HELPER - 1) / HG_HELPER),
                            dim3(128 * HG_HELPER), 0, s, STEP_KARGS(e), a);
+        ++e->n_launch[3];
         return;
     }
 #endif
+    ++e->n_launch[NT ? 4 : 5];
     const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock);
     hipLaunchKernelGGL((step_kernel<T, ETA, NT, FEAT, MULTI, BAKED, NTS>), dim3(grid), dim3(kStepBlock), 0, s,
                        STEP_KARGS(e), a);
@@ -1400,8 +1436,10 @@ static void launch_step(const hg_env* e, hipStream_t s, const StepArgs& a) {
 // next one through the Infinity Cache, plain stores are faster: 37.7 against 38.5 us, 1 M 67.1
 // against 69.4 us); the default airframe's constant-specialised kernel (baked.h) when the env uses
 // it; with or without the optional features.
+// (returns the run-time specialised launch's status; the library's own launches report through
+// hipGetLastError)
 template <int T, bool MULTI>
-static void dispatch_step(const hg_env* e, hipStream_t s, const StepArgs& a, bool eta, bool feat) {
+static hipError_t dispatch_step(const hg_env* e, hipStream_t s, const StepArgs& a, bool eta, bool feat) {
     if (!MULTI && !eta && e->rtc) {   // the airframe's run-time specialised kernels, same size rules
         const int v = e->n <= HG_NT_WAVES * e->resident_envs ? 0 : (e->n <= HG_NTS_WAVES * e->resident_envs ? 2 : 4);
         float* state = e->state;
@@ -1412,8 +1450,8 @@ static void dispatch_step(const hg_env* e, hipStream_t s, const StepArgs& a, boo
         StepArgs args = a;
         void* params[] = {&state, &n, &seed, &off, &pa, &tp, &args};
         const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock);
-        (void)hipModuleLaunchKernel(e->rtc_fn[v + (feat ? 1 : 0)], grid, 1, 1, kStepBlock, 1, 1, 0, s, params, nullptr);
-        return;
+        ++e->n_launch[2];
+        return hipModuleLaunchKernel(e->rtc_fn[v + (feat ? 1 : 0)], grid, 1, 1, kStepBlock, 1, 1, 0, s, params, nullptr);
     }
     auto pick = [&](auto nt) {
         constexpr bool NT = decltype(nt)::value;
@@ -1432,21 +1470,23 @@ static void dispatch_step(const hg_env* e, hipStream_t s, const StepArgs& a, boo
     };
     if (e->n <= HG_NT_WAVES * e->resident_envs) pick(std::true_type{});
     else pick(std::false_type{});
+    return hipSuccess;
 }
 template <bool MULTI>
-static void dispatch_task(const hg_env* e, hipStream_t s, const StepArgs& a, bool eta, bool feat) {
+static hipError_t dispatch_task(const hg_env* e, hipStream_t s, const StepArgs& a, bool eta, bool feat) {
     switch (e->cfg.task) {
-        case HG_TASK_HOVER: dispatch_step<HG_TASK_HOVER, MULTI>(e, s, a, eta, feat); break;
-        case HG_TASK_FORWARD_FLIGHT: dispatch_step<HG_TASK_FORWARD_FLIGHT, MULTI>(e, s, a, eta, feat); break;
-        default: dispatch_step<HG_TASK_HELI, MULTI>(e, s, a, eta, feat); break;
+        case HG_TASK_HOVER: return dispatch_step<HG_TASK_HOVER, MULTI>(e, s, a, eta, feat);
+        case HG_TASK_FORWARD_FLIGHT: return dispatch_step<HG_TASK_FORWARD_FLIGHT, MULTI>(e, s, a, eta, feat);
+        default: return dispatch_step<HG_TASK_HELI, MULTI>(e, s, a, eta, feat);
     }
 }
 
 // ov mode's launch: `ov_trim_blocks` trim blocks (the previous step's ends; blocks without a job exit at
-// once) ahead of the step's blocks
+// once) ahead of the step's blocks -- never more than one per env (a step ends at most n episodes)
 static inline int32_t ov_trim_blocks(int64_t n) {
-    const int64_t b = n / 256;
-    return (int32_t)(b < 64 ? 64 : (b > 1024 ? 1024 : b));
+    int64_t b = n / 256;
+    b = b < 64 ? 64 : (b > 1024 ? 1024 : b);
+    return (int32_t)(b < n ? b : n);
 }
 static void launch_step_ov(const hg_env* e, hipStream_t s, const StepArgs& a, const hgk::RetrimArgs& r) {
     const int32_t tb = ov_trim_blocks(e->n);
@@ -1559,7 +1599,10 @@ static std::vector<float2> split_terrain(const double* t, int32_t rows, int32_t 
 
 // every device resource of a handle (create's error paths and hg_destroy), then the handle
 static void release(hg_env* e) {
-    if (e->rtc_mod) (void)hipModuleUnload(e->rtc_mod);
+    if (e->rtc_mod) {   // steps still queued on any stream may use its kernels
+        (void)hipDeviceSynchronize();
+        (void)hipModuleUnload(e->rtc_mod);
+    }
     dfree(e->hmap); dfree(e->state); dfree(e->az); dfree(e->tmpl_dev); dfree(e->params_dev);
     dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_recs);
     dfree(e->retrim_count); dfree(e->retrim_ring); dfree(e->ov_recs); dfree(e->ov_ring);
@@ -1703,6 +1746,26 @@ int32_t hg_load_specialized(hg_env* e, const char* code_object, int32_t task, co
         if (err != hipSuccess) {
             (void)hipModuleUnload(mod);
             return fail(HG_E_HIP, std::string("hg_load_specialized: ") + names[k] + ": " + hipGetErrorString(err));
+        }
+    }
+    {   // the image and task the code object was built with (step_rtc.hip): a code object built from a
+        // truncated or foreign constant file is refused instead of stepping with its constants
+        hipDeviceptr_t gi = nullptr, gt = nullptr;
+        size_t bi = 0, bt = 0;
+        Params<float> built;
+        int32_t built_task = -1;
+        hipError_t err = hipModuleGetGlobal(&gi, &bi, mod, "hg_rtc_image");
+        if (err == hipSuccess) err = hipModuleGetGlobal(&gt, &bt, mod, "hg_rtc_task");
+        if (err == hipSuccess && (bi != sizeof(built) || bt != sizeof(built_task))) err = hipErrorInvalidValue;
+        if (err == hipSuccess) err = hipMemcpy(&built, gi, sizeof(built), hipMemcpyDeviceToHost);
+        if (err == hipSuccess) err = hipMemcpy(&built_task, gt, sizeof(built_task), hipMemcpyDeviceToHost);
+        if (err != hipSuccess) {
+            (void)hipModuleUnload(mod);
+            return fail(HG_E_HIP, std::string("hg_load_specialized: reading the built image: ") + hipGetErrorString(err));
+        }
+        if (memcmp(&built, image, sizeof(built)) != 0 || built_task != task) {
+            (void)hipModuleUnload(mod);
+            return fail(HG_E_INVALID, "hg_load_specialized: the code object was built with another constant image or task");
         }
     }
     HIP_TRY(hipDeviceSynchronize());   // queued steps may still use a previous module
@@ -1854,7 +1917,9 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.ov_active = ov_active ? 1 : 0;
     const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next ||
                       e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
+    ++e->n_launch[0];
     if (ov_active) {   // the previous step's ends trimmed in this launch's first blocks
+        ++e->n_launch[1];
         const int prev = rt_slot == 0 ? 2 : rt_slot - 1;
         hgk::RetrimArgs r;
         memset(&r, 0, sizeof(r));
@@ -1873,7 +1938,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.tmpl_env = e->Pf.env_templates ? e->tmpl_env : nullptr;
         launch_step_ov(e, s, a, r);
     } else {
-        dispatch_task<false>(e, s, a, eta != nullptr, feat);
+        HIP_TRY(dispatch_task<false>(e, s, a, eta != nullptr, feat));
     }
     HIP_TRY(hipGetLastError());
     if (ov) e->ov_chain = key;
@@ -1950,7 +2015,7 @@ int32_t hg_rollout(hg_env* e, const float* actions, int32_t nsteps, float* obs, 
     hipStream_t s = (hipStream_t)stream;
     const bool feat = e->Pf.autoreset_next || e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates ||
                       e->Pf.reset_retrim;
-    dispatch_task<true>(e, s, a, eta != nullptr, feat);
+    HIP_TRY(dispatch_task<true>(e, s, a, eta != nullptr, feat));
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }
@@ -2083,6 +2148,12 @@ int32_t hg_debug_queues(hg_env* e, int32_t* out) {
     return HG_OK;
 }
 
+int32_t hg_debug_launches(const hg_env* e, int64_t* out) {
+    if (!e || !out) return fail(HG_E_INVALID, "bad env or out");
+    for (int k = 0; k < 6; ++k) out[k] = e->n_launch[k];
+    return HG_OK;
+}
+
 int32_t hg_set_retrim_overlap(hg_env* e, int32_t enable) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
     e->ov_enabled = enable != 0;
@@ -2130,6 +2201,24 @@ int32_t hg_random_actions(hg_env* e, float* actions, uint64_t seed, uint64_t ste
     if ((uintptr_t)actions & 15) return fail(HG_E_INVALID, "actions must be 16-byte aligned");
     hipLaunchKernelGGL(random_actions_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream, actions,
                        e->n, e->cfg.env_offset, seed, step, lo, hi);
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_debug_eta(hg_env* e, float* eta, void* stream) {
+    if (!e || !eta) return fail(HG_E_INVALID, "env/eta is NULL");
+    DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
+    hipLaunchKernelGGL(eta_kernel, dim3(grid_for(e->n)), dim3(kBlock), 0, (hipStream_t)stream, e->state, e->n,
+                       (uint64_t)e->cfg.seed, (int64_t)e->cfg.env_offset, PARAM_ARG(e), eta);
+    HIP_TRY(hipGetLastError());
+    return HG_OK;
+}
+
+int32_t hg_debug_philox(const uint32_t* in, uint32_t* out, int64_t count, void* stream) {
+    if (count < 0 || (count > 0 && (!in || !out))) return fail(HG_E_INVALID, "hg_debug_philox: bad arguments");
+    if (count == 0) return HG_OK;
+    hipLaunchKernelGGL(philox_kernel, dim3(grid_for(count)), dim3(kBlock), 0, (hipStream_t)stream, in, out, count);
     HIP_TRY(hipGetLastError());
     return HG_OK;
 }

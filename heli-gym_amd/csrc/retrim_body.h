@@ -363,9 +363,10 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     const double eps = hg::kTrimEps;
     const int c = l & 15;            // Jacobian column of lanes 0..31
     const int j = l - 32;            // line-search trial of lanes 32..41
-    // the first job record is requested with the job count (the grid never exceeds the list: blocks
-    // <= min(n, 1024)), so the start waits for one load, not two dependent ones
-    const int4 rec0 = a.recs ? a.recs[first] : make_int4(0, 0, 0, 0);
+    // the first job record is requested with the job count, so the start waits for one load, not two
+    // dependent ones; the records hold n entries, and a block past them (a grid of more blocks than
+    // envs) reads none
+    const int4 rec0 = (a.recs && first < a.n) ? a.recs[first] : make_int4(-1, 0, 0, 0);
     int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
 #if HG_RT_DEBUG
     if (l == 0 && first == 0) {   // diagnostic build: one record per launch (count address, jobs, mode, first record)

@@ -23,6 +23,11 @@
         step_body<HG_RTC_TASK, false, NT, FEAT, false, true, NTS>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a, blockIdx.x); \
     }
 
+// the constant image and the task this code object was built with: hg_load_specialized reads them
+// back (hipModuleGetGlobal) and refuses a code object whose image is not the one it is given
+extern "C" __device__ __attribute__((used)) hg::ParamWords hg_rtc_image = __builtin_bit_cast(hg::ParamWords, hg::kBakedAW109);
+extern "C" __device__ __attribute__((used)) int32_t hg_rtc_task = HG_RTC_TASK;
+
 // names and order: hg_load_specialized (heligym_amd.hip) looks them up by these names
 HG_RTC_KERNEL(hg_rtc_step_nt, true, false, false)
 HG_RTC_KERNEL(hg_rtc_step_nt_feat, true, true, false)

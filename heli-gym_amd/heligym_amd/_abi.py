@@ -108,7 +108,10 @@ _SIGS = {
     "hg_set_retrim_overlap": (ctypes.c_int32, [_P, ctypes.c_int32]),
     "hg_debug_retrim_invalid": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "hg_debug_queues": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int32)]),
+    "hg_debug_launches": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "hg_clock_stamp": (ctypes.c_int32, [_P, _P]),
+    "hg_debug_eta": (ctypes.c_int32, [_P, _P, _P]),
+    "hg_debug_philox": (ctypes.c_int32, [_P, _P, ctypes.c_int64, _P]),
     "hg_trim_conds_batch": (ctypes.c_int32, [_P, ctypes.POINTER(hg_trim_cond), ctypes.c_int64, _P, _P, _P, _P,
                                              _P, _P]),
     "hg_set_reset_templates": (ctypes.c_int32, [_P, _P, _P]),

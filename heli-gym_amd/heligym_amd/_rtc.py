@@ -13,6 +13,7 @@ import ctypes
 import hashlib
 import os
 import subprocess
+import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
@@ -68,14 +69,21 @@ def build(lib, cfg, rows, cols, task):
     d = cache_dir()
     path = os.path.join(d, f"step_{key}.hsaco")
     if not os.path.exists(path):
-        inc = os.path.join(d, f"step_{key}.inc")
+        # every file of a build is this process's own (pid-unique names): concurrent builders of the
+        # same key (the ranks of a sharded env) never read a constant file another one is writing
+        tag = f"{os.getpid()}.{threading.get_ident()}"
+        inc = os.path.join(d, f"step_{key}.{tag}.inc")
         with open(inc, "w") as f:
             f.write(render(img))
-        tmp = f"{path}.{os.getpid()}.tmp"
+        tmp = f"{path}.{tag}.tmp"
         cmd = [HIPCC, *FLAGS, "--genco", f'-DHG_BAKED_INC="{inc}"', f"-DHG_RTC_TASK={int(task)}", "-o", tmp,
                os.path.join(CSRC, "step_rtc.hip")]
-        r = subprocess.run(cmd, capture_output=True, text=True)
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True)
+        finally:
+            os.unlink(inc)
         if r.returncode != 0:
             raise RuntimeError(f"step specialisation failed ({' '.join(cmd)}):\n{r.stderr[-2000:]}")
         os.replace(tmp, path)   # atomic: concurrent builders of the same key agree
+    # (hg_load_specialized also checks the image the code object was built with against img)
     return path, img

@@ -599,11 +599,30 @@ class HeliVecEnv(*_VEC_BASES):
         self._check(self.lib.hg_retrim_failures(self._h, ctypes.byref(c)))
         return c.value
 
+    LAUNCH_KINDS = ("steps", "overlapped_retrim", "specialized", "helper", "lone_wave", "bulk")
+
+    def debug_launches(self):
+        """Diagnostic: host-side launch counts of this env (hg_debug_launches): step calls, steps that
+        held the previous step's re-trims, and the kernel kinds that ran."""
+        out = (ctypes.c_int64 * 6)()
+        self._check(self.lib.hg_debug_launches(self._h, out))
+        return dict(zip(self.LAUNCH_KINDS, (int(v) for v in out)))
+
     def retrim_invalid_jobs(self):
         """Diagnostic: re-trim job records that named no env (skipped); 0 in a correct run."""
         c = ctypes.c_int64()
         self._check(self.lib.hg_debug_retrim_invalid(self._h, ctypes.byref(c)))
         return c.value
+
+    def debug_eta(self, out=None):
+        """Diagnostic: the turbulence noise [N,3] (scaled by 1/sqrt(dt), wind_dynamics.py:49-52) each
+        env's next step draws in-kernel, from its current counters (hg_debug_eta).  Injecting it as
+        `eta` gives bitwise the in-kernel step."""
+        t = self.torch
+        if out is None:
+            out = t.empty((self.num_envs, 3), dtype=t.float32, device=self.device)
+        self._check(self.lib.hg_debug_eta(self._h, _ptr(out), self._stream()))
+        return out
 
     def random_actions(self, out, seed, step, lo=-1.0, hi=1.0):
         self._check(self.lib.hg_random_actions(self._h, _ptr(out), int(seed), int(step), float(lo),

@@ -302,6 +302,13 @@ int32_t hg_debug_retrim_invalid(hg_env* env, int64_t* count);
  * re-trim ring or -7, out[6..8] hg_reset's job count, failures, invalid jobs).  Synchronises. */
 int32_t hg_debug_queues(hg_env* env, int32_t* out);
 
+/* Diagnostic: host-side launch counts of this handle since creation: out[0] step calls (hg_step,
+ * hg_step_chained, hg_step_rows), out[1] steps whose launch held the previous step's re-trims
+ * (hg_set_retrim_overlap), out[2] run-time specialised kernel launches, out[3] small-batch helper
+ * kernel launches, out[4] lone-wave (one or two waves per SIMD) launches, out[5] bulk launches
+ * (out[3..5] count hg_rollout's too).  Host only. */
+int32_t hg_debug_launches(const hg_env* env, int64_t* out);
+
 /* HG_RESET_RETRIM with next-step auto-reset (gymnasium's default, make_vec's): the episodes a step ends
  * are re-trimmed (helicopter.py:208-212 -> helicopter_dynamics.py:491-555) while the next step runs,
  * in the same kernel launch as that step (its first blocks), so the caller's stream sees every step
@@ -328,6 +335,17 @@ int32_t hg_set_state(hg_env* env, const float* state_dev, const int32_t* counter
  * (seed, env_offset+i, step).  Not part of the reference surface. */
 int32_t hg_random_actions(hg_env* env, float* actions_dev, uint64_t seed, uint64_t step,
                           float lo, float hi, void* stream);
+
+/* Diagnostic (parity tests): the turbulence noise eta [N,3] fp32 (already scaled by 1/sqrt(dt)) that
+ * each env's next hg_step with eta_dev == NULL draws in-kernel — WindDynamics.step_before
+ * (wind_dynamics.py:49-52) restated as Philox4x32-10 keyed by (seed, env_offset+i, episode step,
+ * episode index) and Box-Muller, computed by the same device function from the env's current
+ * counters.  A step given these values as eta_dev is bitwise the in-kernel step. */
+int32_t hg_debug_eta(hg_env* env, float* eta_dev, void* stream);
+
+/* Diagnostic (known-answer tests): the device Philox4x32-10 on `count` rows of in_dev
+ * {ctr0, ctr1, ctr2, ctr3, key0, key1} (u32) -> out_dev [count,4] u32. */
+int32_t hg_debug_philox(const uint32_t* in_dev, uint32_t* out_dev, int64_t count, void* stream);
 
 /* Benchmark clock: one single-lane kernel on `stream` that writes the GPU's constant 100 MHz clock
  * (s_memrealtime) to dst_dev[0] when it runs.  Two stamps around K steps launched (or captured) on

@@ -213,8 +213,10 @@ def test_rtc_code_object_builds(lib, tmp_path, monkeypatch):
     assert os.path.getsize(path) > 10000 and len(img) % 4 == 0
     blob = open(path, "rb").read()
     for name in ("hg_rtc_step_nt", "hg_rtc_step_nt_feat", "hg_rtc_step_nts", "hg_rtc_step_nts_feat",
-                 "hg_rtc_step_bulk", "hg_rtc_step_bulk_feat"):
+                 "hg_rtc_step_bulk", "hg_rtc_step_bulk_feat", "hg_rtc_image", "hg_rtc_task"):
         assert name.encode() in blob
+    # the build's constant file is process-private and removed afterwards
+    assert not [f for f in os.listdir(tmp_path) if f.endswith((".inc", ".tmp"))]
     t = os.path.getmtime(path)
     assert _rtc.build(lib, cfg, 1024, 1024, cfg.task)[0] == path and os.path.getmtime(path) == t   # cached
     # the image is the baked fields of this airframe, not the default one's

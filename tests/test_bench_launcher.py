@@ -57,6 +57,34 @@ def test_gather_obs_headline_is_config5():
     assert "BASELINE config 5" in d["config"]["workload"] and d["config"]["envs_per_gpu"] == 524288
 
 
+def test_config5_failure_keeps_the_headline():
+    """A config-5 rank that raises (e.g. an RCCL error in its first gather): the config-5 child run
+    fails, the headline line still prints, with config5.error and the child's stderr tail."""
+    rc, lines, err = run("--gpus", "2", env={"HG_BENCH_CONFIG5_INJECT": "fail"})
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and "window_s" in d["timing"]
+    assert "failed" in d["config5"]["error"] and any("injected config-5 failure" in ln for ln in d["config5"]["stderr"]["raised"])
+
+
+def test_config5_hang_keeps_the_headline():
+    """A config-5 child that hangs (every rank stuck, e.g. in a captured multi-rank gather): its ranks'
+    watchdog ends them at the limit, and with the watchdog off the parent kills the child run at the
+    limit; either way the headline line prints with config5.error, well inside the driver's limit."""
+    import time
+    for extra, words in (({}, ("failed", "killed")), ({"HG_BENCH_CONFIG5_NO_WATCHDOG": "1"}, ("killed",))):
+        t0 = time.time()
+        rc, lines, err = run("--gpus", "2", "--config5-timeout", "25",
+                             env={"HG_BENCH_CONFIG5_INJECT": "hang", **extra})
+        assert rc == 0, err[-2000:]
+        assert len(lines) == 1
+        d = json.loads(lines[0])
+        assert any(w in d["config5"]["error"] for w in words), d["config5"]
+        assert "window_s" in d["timing"]
+        assert time.time() - t0 < 150
+
+
 def test_world_size_mismatch_fails():
     rc, lines, err = run("--gpus", "2", env={"WORLD_SIZE": "3"})
     assert rc != 0 and not lines and "WORLD_SIZE=3" in err
