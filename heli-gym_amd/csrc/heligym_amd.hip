@@ -84,7 +84,9 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-__device__ __forceinline__ float u01(uint32_t x) {   // (0, 1)
+// ((x >> 8) + 0.5) 2^-24 in fp32: from 2^23 on the + 0.5 rounds to even, so u is in (0, 1] (1 at the top:
+// a zero Box-Muller radius, never a log of 0); tests/philox_ref.py restates it bitwise
+__device__ __forceinline__ float u01(uint32_t x) {
     return ((float)(x >> 8) + 0.5f) * (1.0f / 16777216.0f);
 }
 
@@ -286,7 +288,7 @@ __device__ __forceinline__ void draw_eta(const StepArgs& a, uint64_t seed, int64
         const uint64_t gid = (uint64_t)(env_offset + blk0 + lo);
         const U4 r = philox(U4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)step, (uint32_t)epi},
                             (uint32_t)seed, (uint32_t)(seed >> 32));
-        // Box-Muller.  Radii sqrt(-2 ln u) / sqrt(dt) = sqrt(log2(u) * (-2 ln 2 / dt)) with u in (0, 1)
+        // Box-Muller.  Radii sqrt(-2 ln u) / sqrt(dt) = sqrt(log2(u) * (-2 ln 2 / dt)) with u in (0, 1]
         // from the top 24 bits; angles in revolutions for the hardware sin / cos (v_sin_f32 takes
         // revolutions: sin(2 pi u) = v_sin(u)), u in [1, 2) from the top 23 bits (a whole turn apart)
         const float rk = P.eta_norm * P.eta_norm * -1.38629436111989061f;   // -2 ln 2 / dt

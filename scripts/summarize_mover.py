@@ -1,0 +1,43 @@
+"""Summarise scripts/r05_mover_prof.sh: per mover case, the traced average launch duration, the PMC
+traffic per launch (2 x FETCH_SIZE + WRITE_SIZE, KiB, the gfx950 correction of MI355X_MICROARCH.md)
+and the achieved rate of the 315 bytes per env the step kernel moves.  Writes
+profiles/r05_mover_4m_pmc_summary.json and copies the kernel stats of case 5."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+d, n = sys.argv[1], int(sys.argv[2])
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+out = {"envs": n, "bytes_per_env": 315, "source": "scripts/ubench/mover.hip via scripts/r05_mover_prof.sh", "cases": {}}
+for c, label in (("5", "12 waves per CU (the bulk step kernel's occupancy), no arithmetic"),
+                 ("9", "12 waves per CU, 1 700 VALU per lane between the loads and the stores")):
+    durs = []
+    for f in glob.glob(os.path.join(d, f"trace{c}", "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "mover" in r["Kernel_Name"]:
+                durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    cnt = {}
+    for f in glob.glob(os.path.join(d, f"pmc{c}_*", "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "mover" in r.get("Kernel_Name", ""):
+                cnt.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+    mean = {k: sum(v) / len(v) for k, v in cnt.items()}
+    e = {"label": label, "launches_traced": len(durs)}
+    if durs:
+        avg = sum(durs) / len(durs)
+        e["kernel_avg_us_trace"] = avg / 1e3
+        e["achieved_GBs_315"] = 315 * n / avg
+    if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
+        rd, wr = 2 * mean["FETCH_SIZE"] * 1024, mean["WRITE_SIZE"] * 1024
+        e.update(hbm_read_bytes_per_launch=rd, hbm_write_bytes_per_launch=wr, hbm_bytes_per_launch=rd + wr,
+                 traffic_over_moved=(rd + wr) / (315 * n), moved_read=128 * n, moved_write=187 * n)
+    out["cases"][c] = e
+    stats = glob.glob(os.path.join(d, f"trace{c}", "**", "*kernel_stats.csv"), recursive=True)
+    if stats and c == "5":
+        shutil.copy(stats[0], os.path.join(root, "profiles", "r05_mover_4m_kernel_stats.csv"))
+with open(os.path.join(root, "profiles", "r05_mover_4m_pmc_summary.json"), "w") as f:
+    json.dump(out, f, indent=1)
+print(json.dumps(out, indent=1))

@@ -8,7 +8,7 @@ is fixed whatever the batch or the rank count:
   * Philox4x32-10 (Salmon et al., "Parallel random numbers: as easy as 1, 2, 3", SC'11; the
     Random123 library's philox4x32 with R = 10) on the counter (gid_lo, gid_hi, episode step,
     episode index) with the 64-bit key `seed` (csrc/heligym_amd.hip philox, draw_eta);
-  * Box-Muller: u = ((x >> 8) + 0.5) 2^-24 in (0, 1) from words 0 and 2, angles from the top 23 bits
+  * Box-Muller: u = ((x >> 8) + 0.5) 2^-24 (float32, in (0, 1], see u01) from words 0 and 2, angles from the top 23 bits
     of words 1 and 3 as a fraction of a turn; eta0 = r0 cos(2 pi a1), eta1 = r0 sin(2 pi a1),
     eta2 = r1 cos(2 pi a3), r = sqrt(-2 ln u / dt).
 
@@ -65,8 +65,12 @@ def noise_words(gid, step, epi, seed):
 
 
 def u01(x):
-    """((x >> 8) + 0.5) / 2^24: exact in float32, in (0, 1)."""
-    return ((np.asarray(x, dtype=np.uint32) >> np.uint32(8)).astype(np.float64) + 0.5) / 16777216.0
+    """The kernel's ((float)(x >> 8) + 0.5f) * 2^-24 in float32 arithmetic: the 24-bit integer converts
+    exactly, but from 2^23 on the + 0.5 rounds (to even), so u is in (0, 1] and only half of the
+    upper values sit mid-cell (the device measured this: a float64 restatement differed by one ulp
+    in half the values past 0.5)."""
+    a = (np.asarray(x, dtype=np.uint32) >> np.uint32(8)).astype(np.float32)
+    return ((a + np.float32(0.5)) * np.float32(1.0 / 16777216.0)).astype(np.float64)
 
 
 def turn_frac(x):
@@ -88,8 +92,8 @@ def random_actions_ref(gid, seed, step, lo=-1.0, hi=1.0):
     """hg_random_actions (csrc/heligym_amd.hip random_actions_kernel): Philox on (gid, step) with the
     key seed ^ (0xA511E9B3, 0x63D83595), each word u01 -> lo + (hi - lo) u, one fused multiply-add in
     float32.  Restated in float64 then rounded to float32: for (lo, hi) = (-1, 1) every value is
-    (2k + 1 - 2^24) 2^-24, exact in both, so the restatement is bitwise (other bounds could differ by
-    a double rounding)."""
+    -1 + 2u with u a multiple of 2^-25 in (0, 1], exact in both, so the restatement is bitwise (other
+    bounds could differ by a double rounding)."""
     gid = np.asarray(gid, dtype=np.int64).astype(np.uint64)
     n = len(gid)
     rows = np.empty((n, 6), dtype=np.uint64)
