@@ -72,9 +72,12 @@ struct U4 {
     uint32_t x, y, z, w;
 };
 
+#ifndef HG_PHILOX_ROUNDS   // (A/B builds only: the library's noise stream is Philox4x32-10)
+#define HG_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-    for (int i = 0; i < 10; ++i) {
+    for (int i = 0; i < HG_PHILOX_ROUNDS; ++i) {
         const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
         const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
         c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};

@@ -28,8 +28,8 @@
 
 #include "physics.h"
 
-#ifndef HG_GEAR_FACTORED   // 1: the landing-gear loads in factored form (see tail of the stage); 0: per point
-#define HG_GEAR_FACTORED 1
+#ifndef HG_GEAR_FACTORED   // the landing-gear loads (gear_add): 3 factored over the gear's mirrored geometry with
+#define HG_GEAR_FACTORED 3   // per-point selects; 1 factored, per-point branches (round 4); 2 moment only; 0 per point
 #endif
 #ifndef HG_MID_ANGLE_MRAD   // largest stage attitude increment (mrad) of the long-series angle addition; 0: none
 #define HG_MID_ANGLE_MRAD 250
@@ -69,6 +69,13 @@ struct StepCtx {
     Ground<float> g;      // ground under the committed x, y (F6)
 };
 
+#ifndef HG_ATT_POLY   // 1: one polynomial pair for every increment up to 0.25 rad; 0: round 4's short / long series
+#define HG_ATT_POLY 0
+#endif
+// the stage-increment polynomials of att_step (HG_ATT_POLY)
+constexpr float kAttA1 = -0x1.55552p-3f, kAttA2 = 0x1.107684p-7f;
+constexpr float kAttB1 = -0.5f, kAttB2 = 0x1.55551cp-5f, kAttB3 = -0x1.6b4f4ep-10f;
+
 // The model constants the stages use as packed operands, built once per step.  As instruction
 // operands a pair of constants must sit in a register pair: left to the compiler, each use
 // re-materialises it with two s_mov (which a lone wave issues as slowly as a VALU instruction), so
@@ -83,6 +90,7 @@ struct StepK {
     f2 j0, j2, g_pq, g_qr;   // I^-1 columns for (p', r') and the gyroscopic coefficients
     f2 k1, dl_db1;           // (K1, K1), (DL_DB1, DL_DB1)
     f2 c6, c24;              // (-1/6, -1/6), (1/24, 1/24)
+    f2 aa1, aa2, ab2, ab3;   // the stage-increment polynomials' coefficients (att_step), as pairs
 };
 
 // Packed products whose sign flip or lane swap is an operand modifier of v_pk_fma_f32 (op_sel /
@@ -175,10 +183,19 @@ HD StepK step_k(const Params<float>& P) {
     K.dl_db1 = f2{P.mr_DL_DB1, P.mr_DL_DB1};
     K.c6 = f2{-1.f / 6.f, -1.f / 6.f};
     K.c24 = f2{1.f / 24.f, 1.f / 24.f};
+    K.aa1 = f2{kAttA1, kAttA1};
+    K.aa2 = f2{kAttA2, kAttA2};
+    K.ab2 = f2{kAttB2, kAttB2};
+    K.ab3 = f2{kAttB3, kAttB3};
     if (!PIN) return K;
     pin(K.is0); pin(K.coef); pin(K.inflow_thr); pin(K.inflow); pin(K.hxy); pin(K.zmax); pin(K.zuu);
     pin(K.zuw); pin(K.one_m1); pin(K.mh_h); pin(K.j0); pin(K.j2); pin(K.g_pq); pin(K.g_qr); pin(K.k1);
-    pin(K.dl_db1); pin(K.c6); pin(K.c24);
+    pin(K.dl_db1);
+#if HG_ATT_POLY
+    pin(K.aa1); pin(K.aa2); pin(K.ab2); pin(K.ab3);
+#else
+    pin(K.c6); pin(K.c24);
+#endif
     return K;
 }
 
@@ -273,6 +290,41 @@ HD StepCtx step_ctx(const Params<float>& P, float a0, float a1, float a2, float 
 
 // Attitude of a stage from the committed one by the angle-addition formulas (physics.h
 // attitude_step), on (sin, cos) pairs; a wave with a large stage increment takes the full sincos.
+#if HG_ATT_POLY
+// sin d = d + d^3 (A1 + A2 d^2) and cos d = 1 + d^2 (B1 + d^2 (B2 + B3 d^2)), fitted on |d| <= 0.25 rad:
+// within 0.55 fp32 ulp of sin / cos over that range evaluated in fp32 (the round-4 short series: 1.19
+// ulp at 0.05), so every wave up to 0.25 rad (all but ~1 % of an aged population's waves) takes this
+// one branch-free form; past it the wave takes the full sincos.
+HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
+    const f2 d01 = pp - pp0;   // phi, psi increments
+    const float d2 = th - th0;
+    const f2 q01 = d01 * d01;
+    const f2 sd01 = (d01 * q01) * (K.aa1 + q01 * K.aa2) + d01;
+    const f2 cd01 = q01 * (kAttB1 + q01 * (K.ab2 + q01 * K.ab3)) + 1.f;
+    const float q2 = d2 * d2;
+    const float sd2 = (d2 * q2) * (kAttA1 + q2 * kAttA2) + d2;
+    const float cd2 = q2 * (kAttB1 + q2 * (kAttB2 + q2 * kAttB3)) + 1.f;
+    // (sin, cos)(e + d) = (s, c) cd + (c, -s) sd
+    const f2 A0 = a0.a[0], A1 = a0.a[1], A2 = a0.a[2];
+    Att2 a;
+    a.a[0] = fma_swn_bx(A0, sd01, A0 * cd01.x);
+    a.a[1] = A1 * cd2 + f2{A1.y, -A1.x} * sd2;
+    a.a[2] = fma_swn_by(A2, sd01, A2 * cd01.y);
+    constexpr float kMax = 0.25f;   // (NaN increments: not in range, the full sincos)
+    const bool in = m_fabs(d01.x) <= kMax && m_fabs(d01.y) <= kMax && m_fabs(d2) <= kMax;
+#ifndef HG_ISA_HOT
+    if (wave_any(!in)) {
+        HG_STAGE_FLAG(8);
+        if (!in) {
+            a.a[0] = sincos2(pp.x);
+            a.a[1] = sincos2(th);
+            a.a[2] = sincos2(pp.y);
+        }
+    }
+#endif
+    return a;
+}
+#else
 HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
     const f2 d01 = pp - pp0;   // phi, psi increments
     const float d2 = th - th0;
@@ -329,6 +381,7 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
     }
     return a;
 }
+#endif
 
 // Stage parts that do not read the wind: the kinematics and the landing gear (:385-398).  Inlined in
 // place in every stage; the small-batch kernel forms stage 1's (stage_pre) while a helper wave runs
@@ -397,6 +450,31 @@ HD void gear_add(const Params<float>& P, const StepCtx& c, const X16& s, const A
             }
         }
         const float bx = -s1, by = B22.x, bz = B22.y;
+        const float Ml0 = Ry * bz - Rz * by, Ml1 = Rz * bx - Rx * bz, Ml2 = Rx * by - Ry * bx;
+#elif HG_GEAR_FACTORED == 3
+        // Factored as below, with the gear's own geometry: the reference places the nose wheel at
+        // (x0, 0, zr) and the two mains at (x1, +-y1, zr) (helicopter_dynamics.py:123-126: one
+        // waterline, the mains mirrored about the centre line), so b.r_i = bz zr + bx x_i (+- by y1)
+        // and r_i.(b x omega) = zr uz + x_i ux (+- y1 uy) share their first terms, and the per-point
+        // contact tests are selects (no divergent branch per point).  QUIRK kept: the moment of point
+        // i uses the force accumulated up to it, and only points in contact add a moment.
+        const float bx = -s1, by = B22.x, bz = B22.y;
+        const float ux = by * r - bz * q, uy = bz * p - bx * r, uz = bx * q - by * p;   // b x omega
+        const float x0 = P.lg_loc[0][0], x1 = P.lg_loc[1][0], y1 = P.lg_loc[1][1], zr = P.lg_loc[0][2];
+        const float pz_c = zh + bz * zr, v_c = n2 + zr * uz;
+        const float pz_m = pz_c + bx * x1, v_m = v_c + x1 * ux;
+        const float pz[3] = {pz_c + bx * x0, pz_m + by * y1, pz_m - by * y1};   // pos_z + h
+        const float vz[3] = {v_c + x0 * ux, v_m + y1 * uy, v_m - y1 * uy};      // contact velocity
+        float w[3], S = 0.f;
+#pragma unroll
+        for (int gi = 0; gi < 3; ++gi) {
+            const bool in = -pz[gi] - P.wl_cg_ft < 0.f;
+            const float fz = -(P.lg_C * vz[gi] + P.lg_K * pz[gi]) + (float)kEps;
+            S = in ? S + fz : S;
+            w[gi] = in ? S : 0.f;
+        }
+        const float Rx = (w[1] + w[2]) * x1 + w[0] * x0, Ry = (w[1] - w[2]) * y1, Rz = ((w[0] + w[1]) + w[2]) * zr;
+        const float Fl0 = S * bx, Fl1 = S * by, Fl2 = S * bz;
         const float Ml0 = Ry * bz - Rz * by, Ml1 = Rz * bx - Rx * bz, Ml2 = Rx * by - Ry * bx;
 #elif HG_GEAR_FACTORED
         // Factored: every contact force is fz_i b with b = (-s1, B22) the third DCM column, so the

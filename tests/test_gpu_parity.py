@@ -343,6 +343,7 @@ def test_trajectories_100_steps(torch, tag):
 # same landings with the gear loads per point give 4.6 / 4.6, with only the moment factored 4.5 /
 # 0.8 (profiles/r04_gear_ab.txt).
 CONTACT_KAPPA = 8.0
+CONTACT_P99 = 1.5   # the 99th percentile of the per-step excess, in envelopes (round 4: 0.79 / 1.16)
 
 
 @pytest.mark.parametrize("dt", [0.01, 0.02])
@@ -402,6 +403,9 @@ def test_trajectories_through_contact(torch, dt):
           {k: round(v, 3) for k, v in worst.items()},
           f"; error beyond contract (ii) in envelopes: median {np.median(ev):.3f}, p99 {np.quantile(ev, 0.99):.3f}, "
           f"max {ev.max():.3f}")
+    # the bulk of the distribution, not only its worst step: a regression of the typical contact step
+    # fails here even while the chaotic worst case stays inside CONTACT_KAPPA
+    assert np.median(ev) <= 0.1 and np.quantile(ev, 0.99) <= CONTACT_P99, (np.median(ev), np.quantile(ev, 0.99))
 
 
 def test_reset_template_vs_reference_trim(torch):
