@@ -217,6 +217,17 @@ def pmc_summary(envs, dt, task, need="hbm_bytes_per_launch", tags=None):
     return best
 
 
+def pattern_ceiling():
+    """The committed measurement of the step kernel's own 4 M-env memory pattern with no arithmetic
+    (profiles/r05_mover_4m_pmc_summary.json, scripts/r05_mover_prof.sh), or None."""
+    path = os.path.join(ROOT, "profiles", "r05_mover_4m_pmc_summary.json")
+    try:
+        d = json.load(open(path))
+        return d if "period_us_event_timed" in d else None
+    except (OSError, ValueError):
+        return None
+
+
 def pmc_traffic(envs, dt, task):
     """HBM bytes per step-kernel launch (FETCH_SIZE / WRITE_SIZE passes), or None."""
     r = pmc_summary(envs, dt, task)
@@ -1020,9 +1031,16 @@ def main():
             s_x, _, _, rs_x = timer.run_counted(envx, repx, 3)
             del _kx
             ach = Nx * BYTES_PER_ENV_STEP / (s_x / Kx) / 1e9
+            ceil = pattern_ceiling()
             secondary["out_of_cache"] = {
                 "envs": Nx, "value": Nx * Kx / s_x, "unit": "env-steps/s", "ms_per_step": s_x / Kx * 1e3,
                 "steps": Kx, "achieved_GBs": ach, "frac": ach / HBM_PEAK_GBS,
+                # the step's own memory pattern with the arithmetic taken out (scripts/ubench/mover.hip):
+                # the period this access pattern reaches on the chip, and the step's fraction of it
+                "pattern_ceiling": ceil and {"ms_per_step": ceil["period_us_event_timed"] * 1e-3,
+                                             "GBs_315": ceil["ceiling_GBs_315"],
+                                             "frac_of_ceiling": ceil["period_us_event_timed"] * 1e-3 / (s_x / Kx * 1e3),
+                                             "source": "profiles/r05_mover_4m_pmc_summary.json"},
                 "resets_in_window": rs_x, "aged_steps": aged_x,
                 "traffic": (pmc_traffic(Nx, args.dt, args.task) or (None,))[0],
                 "traffic_source": (pmc_traffic(Nx, args.dt, args.task) or (None, None))[1],

@@ -321,23 +321,36 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
         const int w_ = (int)(i >> 6);                                                           \
         if ((tid & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;                      \
     } while (0)
+// the stamping wave's tile from the hardware ids (the small-batch kernel's blocks are a stepping wave and
+// its helper: the stepping wave is wave 0, its tile the block)
+#define HG_STAMP_WAVE() (blockDim.x == 128 ? (int)blockIdx.x : (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6))
 // the same stamp from inside the RK driver (stage_f32.h), where only the hardware ids are in scope
 #define HG_STAGE_STAMP(j, ...)                                                                  \
     do {                                                                                        \
         asm volatile("" ::__VA_ARGS__);                                                         \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
-        const int w_ = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);                    \
+        const int w_ = HG_STAMP_WAVE();                                                         \
         if ((threadIdx.x & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;              \
     } while (0)
 // which wave-uniform branches the wave took (HG_TIMING builds): 1 reset, 2 gear contact code,
 // 4 the full sincos of a large attitude increment
 #define HG_STAGE_FLAG(bit)                                                                      \
     do {                                                                                        \
-        const int w_ = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);                    \
+        const int w_ = HG_STAMP_WAVE();                                                         \
         if ((threadIdx.x & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][16] |= (bit);         \
+    } while (0)
+// the small-batch kernel's helper waves (one per tile): 0 start (s_memrealtime), 1 start (s_memtime),
+// 2 the tile's counters arrived (noise key), 3 noise and wind step done, 4 past the hand-off barrier
+__device__ unsigned long long g_timing_help[HG_TIMING_WAVES][5];
+#define HSTAMP(j, ...)                                                                          \
+    do {                                                                                        \
+        asm volatile("" ::__VA_ARGS__);                                                         \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                             \
+        if (lane == 0 && tile < HG_TIMING_WAVES) g_timing_help[tile][j] = t_;                   \
     } while (0)
 #else
 #define TSTAMP(j, ...) do { } while (0)
+#define HSTAMP(j, ...) do { } while (0)
 #endif
 
 }  // namespace
@@ -400,19 +413,26 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
             return;
         }
         if (helper) {   // the tile's noise and wind step (Heli.step :195-199), the same code as below
+#if HG_TIMING
+            if (lane == 0 && tile < HG_TIMING_WAVES) g_timing_help[tile][0] = __builtin_amdgcn_s_memrealtime();
+#endif
+            HSTAMP(1, "v"(lane));
             const Params<float>& PH = BAKED ? PB : P0;
             const f32x4 g0 = ld_lane(GRP(st_b, 0), lt), g1 = ld_lane(GRP(st_b, 1), lt), g2 = ld_lane(GRP(st_b, 2), lt),
                         g3 = ld_lane(GRP(st_b, 3), lt);
             float ws[5], carry[4], eta[3], W[3];
             carry[3] = g1.z; carry[0] = g1.w; carry[1] = g2.x; carry[2] = g2.y;
             ws[0] = g2.z; ws[1] = g2.w; ws[2] = g3.x; ws[3] = g3.y; ws[4] = g3.z;
+            HSTAMP(2, "v"(g0.w), "v"(g1.x));
             draw_eta<false>(a, seed_p, envoff_p, PH, 0, blk0, lo, __float_as_int(g0.w), __float_as_int(g1.x), eta);
             hg::wind_step_f32(PH, ws, carry, eta, W);
+            HSTAMP(3, "v"(W[0]), "v"(ws[4]));
             float* sw = s_wind + wv * 8 * 64 + lane;
             sw[0] = W[0]; sw[64] = W[1]; sw[128] = W[2];
 #pragma unroll
             for (int c = 0; c < 5; ++c) sw[(3 + c) * 64] = ws[c];
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            HSTAMP(4, "v"(lane));
             return;
         }
     }
@@ -442,6 +462,13 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
         hs[10] = g6.x; hs[11] = g6.y; hs[12] = g6.z; hs[13] = g6.w;
         hs[2] = 0.f; hs[3] = 0.f;
     }
+#ifndef HG_EARLY_PAIRS   // 1: the stages' constant pairs formed while the state loads are in flight (round 5
+#define HG_EARLY_PAIRS 0  // A/B: 7.062 -> 7.088 us, profiles/r05_valu_ab.txt; not adopted)
+#endif
+#if HG_EARLY_PAIRS
+    // (data-independent: issued ahead of the first wait for the state, off the step's critical path)
+    const hg::StepK Kpairs = hg::step_k<NT && HG_PIN_CONSTANTS>(BAKED ? PB : P0);
+#endif
     if (FEAT && bid == 0 && tid == 0) {   // counters of a later step (rings of three)
         if (a.reset_count_next) *a.reset_count_next = 0;
         if (a.retrim_slot >= 0 && a.retrim_count) a.retrim_count[a.retrim_slot == 2 ? 0 : a.retrim_slot + 1] = 0;
@@ -468,13 +495,20 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
         // while the helper wave runs the wind
         const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
         ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, 0.f, 0.f, 0.f, h_c, hs[17]);
+#if HG_EARLY_PAIRS
+        rk.begin(P, ctx, hs, hg::att0(hs), Kpairs);
+#else
         rk.begin(P, ctx, hs, hg::att0(hs));
+#endif
+        TSTAMP(2, "v"(ctx.z0), "v"(hs[0]));   // (HELP: the wind-independent context and stage-1 share done)
         asm volatile("s_barrier" ::: "memory");
+        TSTAMP(3, "v"(tid));                  // (HELP: past the hand-off barrier)
         const float* sw = s_wind + wv * 8 * 64 + lane;
         W[0] = sw[0]; W[1] = sw[64]; W[2] = sw[128];
 #pragma unroll
         for (int c = 0; c < 5; ++c) ws[c] = sw[(3 + c) * 64];
         ctx.W0 = W[0]; ctx.W1 = W[1]; ctx.W2 = W[2];
+        TSTAMP(4, "v"(W[0]), "v"(ws[4]));     // (HELP: the wind read from LDS)
     } else {
     // turbulence noise (wind_dynamics.py:49-52): injected, or Philox normals
     float eta[3];
@@ -488,7 +522,11 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
 
     TSTAMP(4, "v"(h_c.delta), "v"(h_c.hi));
     ctx = hg::step_ctx(P, act.x, act.y, act.z, act.w, W[0], W[1], W[2], h_c, hs[17]);
+#if HG_EARLY_PAIRS
+    rk.begin(P, ctx, hs, hg::att0(hs), Kpairs);
+#else
     rk.begin(P, ctx, hs, hg::att0(hs));
+#endif
     }
     // RK4 (dynamics.py:158-171); observation from the stage-4 input (F5)
     float k[18], obs[17];
@@ -514,9 +552,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     // (The rotor azimuths' wrap is az_advance's.)
     {
         const int ang[5] = {4, 5, 12, 13, 14};
-        bool all_in = true;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) all_in = all_in && in_pi_range(hs[ang[j]]);
+        // every angle in (-pi, pi) <=> the largest |angle| below fp32 pi (two v_max3 with |.| operand
+        // modifiers and one compare instead of five range tests; a NaN angle drops out of the max
+        // and stays NaN either way)
+        const float amax = fmaxf(fmaxf(fmaxf(fabsf(hs[4]), fabsf(hs[5])), fabsf(hs[12])),
+                                 fmaxf(fabsf(hs[13]), fabsf(hs[14])));
+        const bool all_in = amax < 3.14159274101257324f;
         if (__any(!all_in)) {
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
@@ -1512,6 +1553,9 @@ extern "C" {
 #if HG_TIMING
 int hg_debug_timing(void* dst, int64_t bytes) {
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_timing), (size_t)bytes) == hipSuccess ? 0 : -1;
+}
+int hg_debug_timing_help(void* dst, int64_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_timing_help), (size_t)bytes) == hipSuccess ? 0 : -1;
 }
 #endif
 

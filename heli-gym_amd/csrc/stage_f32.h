@@ -780,9 +780,14 @@ struct RK4Step {
     StepK K;
     StagePre pre1;
     HD void begin(const Params<float>& P, const StepCtx& c, const float* hs, const Att2& a) {
+        begin(P, c, hs, a, step_k<LONE && HG_PIN_CONSTANTS>(P));
+    }
+    // with the constant pairs built by the caller (the step kernel builds them before its state loads
+    // arrive, where a lone wave's pin moves cost nothing: it waits for the loads anyway)
+    HD void begin(const Params<float>& P, const StepCtx& c, const float* hs, const Att2& a, const StepK& k) {
         h = to_x16(hs);
         a0 = a;
-        K = step_k<LONE && HG_PIN_CONSTANTS>(P);
+        K = k;
         if constexpr (PRE1) pre1 = stage_pre(P, c, h, a0);
     }
     HD void finish(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,

@@ -38,6 +38,20 @@ for c, label in (("5", "12 waves per CU (the bulk step kernel's occupancy), no a
     stats = glob.glob(os.path.join(d, f"trace{c}", "**", "*kernel_stats.csv"), recursive=True)
     if stats and c == "5":
         shutil.copy(stats[0], os.path.join(root, "profiles", "r05_mover_4m_kernel_stats.csv"))
+# the event-timed sweep of the same binary (100 launches per hipGraph, profiles/r05_mover_sweep_4m.txt):
+# the launch period of the pattern, comparable with bench.py's per-step period
+sweep = os.path.join(root, "profiles", "r05_mover_sweep_4m.txt")
+if os.path.exists(sweep):
+    rows = []
+    for ln in open(sweep):
+        if "waves/CU 12" in ln:
+            rows.append((int(ln.split("VALU/lane")[1].split(":")[0]), float(ln.split(":")[1].split("us")[0])))
+    if rows:
+        best = min(rows, key=lambda r: r[1])
+        out["period_us_event_timed"] = best[1]
+        out["period_source"] = (f"{sweep[len(root) + 1:]}: the fastest 12-waves-per-CU case ({best[0]} VALU per lane), "
+                                "HIP events over 100-launch graphs")
+        out["ceiling_GBs_315"] = 315 * n / best[1] / 1e3
 with open(os.path.join(root, "profiles", "r05_mover_4m_pmc_summary.json"), "w") as f:
     json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))

@@ -11,7 +11,8 @@ import sys
 # step_kernel<TASK, ETA, NT, FEAT, MULTI, BAKED, NTS>: the per-step launch of the specialised kernel
 # (MULTI false, BAKED true) is the judged kernel; bench.py's generic-kernel secondary figure
 # (BAKED false) and hg_rollout's multi-step launches (MULTI true) are summarised separately.
-SINGLE = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, true(, (true|false))?>")
+SINGLE = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, true(, (true|false))?>"
+                    r"|step_help_kernel<\d+, (true|false), true>")
 GENERIC = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, false(, (true|false))?>")
 MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true, (true|false)(, (true|false))?>")
 
@@ -28,16 +29,19 @@ for f in glob.glob(os.path.join(d, "pmc*", "**", "*counter_collection.csv"), rec
     for r in csv.DictReader(open(f)):
         if SINGLE.search(r.get("Kernel_Name", "")):
             agg.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+names = set()
 for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         if SINGLE.search(r["Kernel_Name"]):
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            names.add(r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", ""))
         elif MULTI.search(r["Kernel_Name"]):
             mdurs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         elif GENERIC.search(r["Kernel_Name"]):
             gdurs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
-out = {"tag": tag, "envs": n, "dt": dt, "task": task, "kernel": "step_kernel<HOVER, BAKED> (specialised)",
+out = {"tag": tag, "envs": n, "dt": dt, "task": task,
+       "kernel": (", ".join(sorted(names)) or "step_kernel<HOVER, BAKED>") + " (specialised)",
        "kernel_avg_ns_trace": sum(durs) / len(durs) if durs else None,
        "launches_traced": len(durs), "counters_per_launch": mean}
 if gdurs:

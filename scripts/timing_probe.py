@@ -15,6 +15,13 @@ PHASES = ["state loads", "philox", "wind step", "ground h_c", "RK stage 1", "RK 
           "RK stage 4 + update", "wraps + template fetch", "reward/flags/post-ground",
           "flag stores + reset + obs stores", "state stores", "store drain"]
 ORDER = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 13, 11, 12]   # stamp slots in program order
+# the small-batch helper kernel's stepping waves (step_help_kernel: slots 2-4 mark the hand-off)
+PHASES_HELP = ["state loads", "context + stage-1 wind-free part", "wait at the hand-off barrier",
+               "wind read from LDS", "RK stage 1", "RK stage 2", "RK stage 3", "RK stage 4 + update",
+               "wraps + template fetch", "reward/flags/post-ground", "flag stores + reset + obs stores",
+               "state stores", "store drain"]
+HELPER = ["helper: state loads (counters, carry, wind state)", "helper: noise + wind step",
+          "helper: LDS hand-off + barrier"]
 
 
 def main():
@@ -49,7 +56,22 @@ def main():
     print(f"wave start spread: p50 {np.median(starts)/1e3:.2f} us p90 {np.percentile(starts, 90)/1e3:.2f} "
           f"max {starts.max()/1e3:.2f} us; last wave end {ends.max()/1e3:.2f} us")
     d = np.diff(t, axis=1).astype(np.float64) / ghz / 1e3   # us
-    for j, name in enumerate(PHASES):
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    helper = args.envs <= 64 * 4 * cus // 2   # heligym_amd.hip launch_step: HG_HELPER_DIV = 2
+    if helper:
+        hb = np.zeros((2048, 5), dtype=np.uint64)
+        fh = env.lib.hg_debug_timing_help
+        fh.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+        assert fh(hb.ctypes.data, hb.nbytes) == 0
+        h = hb[:nw].astype(np.int64)
+        hd = np.diff(h[:, 1:5], axis=1).astype(np.float64) / ghz / 1e3
+        hstart = (h[:, 0] - rt[:, 1].min()) * 10.0
+        print(f"helper waves: start p50 {np.median(hstart)/1e3:.2f} us (stepping waves {np.median(starts)/1e3:.2f}); "
+              f"life to the barrier median {np.median((h[:, 4] - h[:, 1]) / ghz) / 1e3:.2f} us")
+        for j, name in enumerate(HELPER):
+            print(f"  {name:48s} median {np.median(hd[:, j]):6.3f} us   p90 {np.percentile(hd[:, j], 90):6.3f} us")
+        print("stepping waves:")
+    for j, name in enumerate(PHASES_HELP if helper else PHASES):
         print(f"  {name:24s} median {np.median(d[:, j]):6.3f} us   p90 {np.percentile(d[:, j], 90):6.3f} us   "
               f"max {d[:, j].max():6.3f} us")
     # which wave-uniform branches the waves took, and how long those waves lived
