@@ -1223,7 +1223,7 @@ hg::TrimSetup trim_setup(const Params<double>& P, const float2* hmap, const hg_t
 // HelicopterDynamics.trim (helicopter_dynamics.py:491-555), serial: fp64 Newton with a central-
 // difference Jacobian and step halving, the reference's iteration logic.
 int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond& tc, const double W[3],
-                hg_trim_result* out) {
+                hg_trim_result* out, double* jac_rec = nullptr, int32_t jac_max = 0, int32_t* jac_n = nullptr) {
     const hg::TrimSetup T = trim_setup(P, hmap, tc);
     const double eps = hg::kTrimEps;
     double x[16], y[16];
@@ -1241,6 +1241,10 @@ int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond&
             hg::trim_fcn(P, T, xp, W, yp, nullptr, nullptr, nullptr);
             hg::trim_fcn(P, T, xm, W, ym, nullptr, nullptr, nullptr);
             for (int k = 0; k < 16; ++k) J[k][i] = (yp[k] - ym[k]) / (2 * eps);
+        }
+        if (jac_rec && jac_n && *jac_n < jac_max) {   // (hg_debug_trim_jacobians)
+            memcpy(jac_rec + (size_t)(*jac_n) * 256, J, sizeof(J));
+            ++*jac_n;
         }
         for (int k = 0; k < 16; ++k) r[k] = y[k] - T.yt[k];
         if (!hg::solve16(J, r, dir)) return fail(HG_E_TRIM, "trim: singular Jacobian");
@@ -1657,6 +1661,24 @@ static void release(hg_env* e) {
     dfree(e->retrim_count); dfree(e->retrim_ring); dfree(e->ov_recs); dfree(e->ov_ring);
     dfree(e->tmpl_env); dfree(e->setup_batch);
     delete e;
+}
+
+// Diagnostic (not in the header): the host trim's central-difference Jacobian of every Newton step
+// (row-major [k][16][16] into jac, at most jac_max), for studying the solve offline.  Returns the
+// number recorded, or an HG_E_* code.
+int32_t hg_debug_trim_jacobians(const hg_config* cfg, const double* terrain_ft, int32_t rows, int32_t cols,
+                                const double wind_ned[3], double* jac, int32_t jac_max) {
+    int32_t rc = check_config(cfg, rows, cols);
+    if (rc != HG_OK) return rc;
+    if (!terrain_ft || !jac || jac_max < 1) return fail(HG_E_INVALID, "bad arguments");
+    const Params<double> P = derive<double>(*cfg, rows, cols);
+    double W[3] = {P.wm[0], P.wm[1], P.wm[2]};
+    if (wind_ned) { W[0] = wind_ned[0]; W[1] = wind_ned[1]; W[2] = wind_ned[2]; }
+    const std::vector<float2> hm = split_terrain(terrain_ft, rows, cols);
+    hg_trim_result out;
+    int32_t n = 0;
+    rc = do_trim(P, hm.data(), cfg->trim, W, &out, jac, jac_max, &n);
+    return rc == HG_OK ? n : rc;
 }
 
 int32_t hg_trim(const hg_config* cfg, const double* terrain_ft, int32_t rows, int32_t cols,
