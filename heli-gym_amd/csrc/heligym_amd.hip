@@ -80,7 +80,13 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
     for (int i = 0; i < HG_PHILOX_ROUNDS; ++i) {
         const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
         const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+#ifndef HG_NO_BITOP3
+        // hi ^ y ^ k as one three-input bitwise instruction (truth table 0x96 = XOR3)
+        c = U4{(uint32_t)__builtin_amdgcn_bitop3_b32(hi1, c.y, k0, 0x96), lo1,
+               (uint32_t)__builtin_amdgcn_bitop3_b32(hi0, c.w, k1, 0x96), lo0};
+#else
         c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+#endif
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
     }
@@ -785,14 +791,14 @@ __global__ __launch_bounds__(128 * HG_HELPER, 1) void step_help_kernel(float* __
 // two waves per SIMD (<= 256 VGPRs), so at one step wave per SIMD a trim wave shares a SIMD with a
 // step wave; the trims, dispatched first, are the long pole.  One queue and no cross-stream events:
 // dependent work on another queue waited about 10 us per hop on MI355X (scripts/r04_ov_trace.py).
-// retrim_jobs treats threadIdx.x as the lane of a single wave (Jacobian column, trial, LDS rows)
-static_assert(kStepBlock == 64, "step_ov_kernel's trim blocks are one wave");
 template <int TASK, bool BAKED>
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2))) void step_ov_kernel(
     float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p, ParamArg Pa,
     const Template<float>* __restrict__ Tp, const StepArgs a, const hgk::RetrimArgs r, int32_t tb) {
     if ((int32_t)blockIdx.x < tb) {
-        hgk::retrim_jobs(r, blockIdx.x, tb);
+        // retrim_jobs treats threadIdx.x as the lane of one wave (Jacobian column, trial, LDS rows):
+        // a trim block is its first wave (the others, with HG_STEP_BLOCK > 64, leave at once)
+        if (kStepBlock == 64 || threadIdx.x < 64) hgk::retrim_jobs(r, blockIdx.x, tb);
         return;
     }
     step_body<TASK, false, true, true, false, BAKED, false>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a,

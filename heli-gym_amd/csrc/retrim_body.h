@@ -341,6 +341,18 @@ __device__ __forceinline__ const T& opaque_const(const T* p) {
     return *(const T*)c;
 }
 
+// HG_RT_XLDS: the Newton iterate x and direction dir (uniform over the wave) live in LDS instead of
+// 64 VGPRs, which leaves the solve's schedule room to keep its lane shuffles in flight
+#ifndef HG_RT_XLDS
+#define HG_RT_XLDS 1
+#endif
+#if HG_RT_XLDS
+#define HG_X(k) sXc[k]
+#define HG_DIR(k) sX[k]
+#else
+#define HG_X(k) x[k]
+#define HG_DIR(k) dir[k]
+#endif
 #ifndef HG_RETRIM_WAVES
 #define HG_RETRIM_WAVES 2
 #endif
@@ -356,6 +368,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     __shared__ double sE[42 * kEStride];   // rows 32..41: the line-search trials' evaluations
     __shared__ double sYt[16];       // the trim's target derivatives y* (its right-hand side is y(src) - y*)
     __shared__ double sX[16];        // the solution (Newton direction), by column
+    __shared__ double sXc[HG_RT_XLDS ? 16 : 1];   // HG_RT_XLDS: the current iterate
     __shared__ double sExt[7];       // observation terms of the current iterate
     __shared__ double sRow[HG_GJ_LDS ? 64 * kRowStride : 2];   // HG_GJ_LDS: the rows of the solve
     const int l = threadIdx.x;
@@ -407,10 +420,18 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             W[1] = (double)wr[1];
             W[2] = (double)wr[2];
         }
-        double x[16], dir[16], ye[16], te = 0.0;
+        double ye[16], te = 0.0;
         EvalExt ext;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; ye[k] = 0.0; }
+        for (int k = 0; k < 16; ++k) ye[k] = 0.0;
+#if HG_RT_XLDS
+        if (l < 16) { sXc[l] = T.x0[l]; sX[l] = 0.0; }
+        lds_order();
+#else
+        double x[16], dir[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; }
+#endif
         double tol = 0;
         int it = 0, kind = kRoundFirst, src = 32, round = 0;
         bool ok = true, converged = false;
@@ -429,7 +450,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             double xe[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
-                const double b = fma(-sl, dir[k], x[k]);
+                const double b = fma(-sl, HG_DIR(k), HG_X(k));
                 xe[k] = (l < 32 && c == k) ? b + pe : b;
             }
             RSTAMP(1 + 4 * round, "v"(xe[0]));
@@ -458,8 +479,13 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                     const int js = lower ? __builtin_ctzll(lower) : hg::kTrimLineSearch;
                     if (js >= hg::kTrimLineSearch - 1) break;   // helicopter_dynamics.py:540: keep x
                     const double step = ldexp(1.0, -js);
+#if HG_RT_XLDS
+                    if (l < 16) sXc[l] = fma(-step, sX[l], sXc[l]);
+                    lds_order();
+#else
 #pragma unroll
                     for (int k = 0; k < 16; ++k) x[k] = fma(-step, dir[k], x[k]);
+#endif
                     src = 32 + js;
                     have_jac = js == 0;   // the Jacobian lanes evaluated around trial 0
                     if (++it > hg::kTrimMaxIter) { ok = false; break; }
@@ -515,8 +541,12 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                 bool fin = true;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
+#if HG_RT_XLDS
+                    fin = fin && isfinite(sX[k]);
+#else
                     dir[k] = sX[k];
                     fin = fin && isfinite(dir[k]);
+#endif
                 }
                 if (!fin) { ok = false; break; }
             }
@@ -541,17 +571,26 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                 bool fin = true;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
+#if HG_RT_XLDS
+                    fin = fin && isfinite(sX[k]);
+#else
                     dir[k] = sX[k];
                     fin = fin && isfinite(dir[k]);
+#endif
                 }
                 if (!fin) { ok = false; break; }
             }
 #endif
-            RSTAMP(4 + 4 * round, "v"(dir[0]));
+            RSTAMP(4 + 4 * round, "v"(HG_DIR(0)));
             kind = kRoundNormal;
             ++round;
         }
         RSTAMP(63, "v"(l));
+#if HG_RT_XLDS
+        double x[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = sXc[k];
+#endif
         if (ok) {
             if (converged) {
                 if (l == src) retrim_write(a, P, T, job, env, x, ext.o);

@@ -13,7 +13,7 @@
 // LDS_PAD caps the resident waves per CU (the step's bulk variant runs three waves per SIMD, 12 per
 // CU) by giving each one-wave block that much dynamic LDS.
 // Usage: mover [N] -> per launch time (100 launches per hipGraph, HIP events) and achieved GB/s of the
-// 315 bytes per env, for BURN in {0, 400, 800, 1200, 1700} x {unrestricted, 12 waves per CU}.
+// 315 bytes per env, for BURN in {0, 400, 800, 1200, 1700} x {unrestricted, 12, 8, 16 waves per CU}.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -112,10 +112,13 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&state, 112 * n)); CK(hipMalloc(&act, 16 * n)); CK(hipMalloc(&obs, 68 * n));
     CK(hipMalloc(&rew, 4 * n)); CK(hipMalloc(&fl, 3 * n));
     CK(hipMemset(state, 0, 112 * n)); CK(hipMemset(act, 0, 16 * n));
-    // 12 one-wave blocks per CU: 160 KB / 12 of LDS each (the kernel's static 4 352 B included)
-    const size_t pad12 = 160 * 1024 / 12 - 64 * 17 * 4;
+    // W one-wave blocks per CU: 160 KB / W of LDS each (the kernel's static 4 352 B included); the
+    // cases keep their round-5 indices (unrestricted 0-4, 12 per CU 5-9), 8 and 16 per CU follow
+    auto pad_for = [](int w) { return (size_t)(160 * 1024 / w - 64 * 17 * 4); };
     int idx = 0;
-    for (size_t pad : {(size_t)0, pad12}) {
+    const int wpc[4] = {0, 12, 8, 16};
+    for (int wi = 0; wi < 4; ++wi) {
+        const size_t pad = wpc[wi] ? pad_for(wpc[wi]) : 0;
         double us[5];
         int rc = 0;
         const int burns[5] = {0, 400, 800, 1200, 1700};
@@ -129,8 +132,10 @@ int main(int argc, char** argv) {
                 default: rc = run<1700>(st, n, pad, state, act, obs, rew, fl, &us[b]); break;
             }
             if (rc) return rc;
+            char wl[8];
+            snprintf(wl, sizeof wl, "%d", wpc[wi]);
             printf("N=%lld waves/CU %-5s VALU/lane %4d: %8.2f us/launch  %7.1f GB/s (315 B/env)  %7.1f GB/s (318 B/env)\n",
-                   (long long)n, pad ? "12" : "max", burns[b], us[b], 315.0 * n / us[b] * 1e-3, 318.0 * n / us[b] * 1e-3);
+                   (long long)n, wpc[wi] ? wl : "max", burns[b], us[b], 315.0 * n / us[b] * 1e-3, 318.0 * n / us[b] * 1e-3);
             fflush(stdout);
         }
     }
