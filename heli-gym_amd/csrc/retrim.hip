@@ -12,6 +12,12 @@
 // device library anyway); the tests hold the device trims to it and to the reference's recorded
 // resets at fp32 resolution.
 #include "../../include/heligym_amd.h"
+// The iterate stays in registers here (retrim_body.h HG_RT_XLDS, bitwise either way): in LDS it
+// helps the overlapped launch, whose step waves share the SIMDs, and costs this kernel 0.3 us per
+// re-trim step.
+#ifndef HG_RT_XLDS
+#define HG_RT_XLDS 0
+#endif
 #include "retrim_body.h"
 
 namespace hgk {

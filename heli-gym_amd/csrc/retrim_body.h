@@ -353,6 +353,9 @@ __device__ __forceinline__ const T& opaque_const(const T* p) {
 #define HG_X(k) x[k]
 #define HG_DIR(k) dir[k]
 #endif
+#ifndef HG_RT_VLOAD
+#define HG_RT_VLOAD 1
+#endif
 #ifndef HG_RETRIM_WAVES
 #define HG_RETRIM_WAVES 2
 #endif
@@ -374,13 +377,34 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     const int l = threadIdx.x;
     const hg::Params<double>& P = *a.P;
     const double eps = hg::kTrimEps;
+#if HG_TIMING
+    if (l == 0 && first == 0) g_rt_timing[62] = __builtin_amdgcn_s_memtime();   // entry (start-up latency)
+#endif
     const int c = l & 15;            // Jacobian column of lanes 0..31
     const int j = l - 32;            // line-search trial of lanes 32..41
     // the first job record is requested with the job count, so the start waits for one load, not two
     // dependent ones; the records hold n entries, and a block past them (a grid of more blocks than
     // envs) reads none
+#if HG_RT_VLOAD
+    // the job count and the first record as vector loads (a uniform address made opaque to the
+    // compiler), both requested before either is waited for: as scalar loads each was waited for at
+    // once (its result spills to VGPR lanes), two memory latencies in a row.  A block with nothing to
+    // read reads the model constants instead (any readable address) and discards them.
+    int zero_v;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zero_v));
+    const bool has_rec0 = a.recs && first < a.n;
+    const int4 rec0_v = (has_rec0 ? a.recs + first : reinterpret_cast<const int4*>(a.P))[zero_v];
+    const int32_t count_v = (a.count ? a.count : reinterpret_cast<const int32_t*>(a.P))[zero_v];
+#endif
+#if HG_RT_VLOAD
+    const int4 rec0 = has_rec0 ? make_int4(__builtin_amdgcn_readfirstlane(rec0_v.x), __builtin_amdgcn_readfirstlane(rec0_v.y),
+                                           __builtin_amdgcn_readfirstlane(rec0_v.z), __builtin_amdgcn_readfirstlane(rec0_v.w))
+                               : make_int4(-1, 0, 0, 0);
+    int64_t jobs = a.count ? (int64_t)__builtin_amdgcn_readfirstlane(count_v) : a.njobs;
+#else
     const int4 rec0 = (a.recs && first < a.n) ? a.recs[first] : make_int4(-1, 0, 0, 0);
     int64_t jobs = a.count ? (int64_t)*a.count : a.njobs;
+#endif
 #if HG_RT_DEBUG
     if (l == 0 && first == 0) {   // diagnostic build: one record per launch (count address, jobs, mode, first record)
         const unsigned k = atomicAdd(&g_rt_dbg_n, 1u);

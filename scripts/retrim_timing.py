@@ -26,6 +26,8 @@ def main():
     t = buf.astype(np.int64)
     ghz = 2.2
     print(f"total {(t[63] - t[0]) / ghz / 1e3:.2f} us (at {ghz} GHz)")
+    if t[62] > 0:   # kernel entry -> the first job's start (job count, record, trim setup)
+        print(f"start-up {(t[0] - t[62]) / ghz / 1e3:.2f} us")
     r = 0
     while 4 + 4 * r < 63 and t[1 + 4 * r] > 0 and t[4 + 4 * r] > 0:
         e = (t[2 + 4 * r] - t[1 + 4 * r]) / ghz / 1e3
