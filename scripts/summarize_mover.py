@@ -9,11 +9,16 @@ import os
 import shutil
 import sys
 
-d, n = sys.argv[1], int(sys.argv[2])
+d, n = sys.argv[1], int(sys.argv[2])   # d = "-": keep the committed PMC cases, update the period only
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+summary = os.path.join(root, "profiles", "r05_mover_4m_pmc_summary.json")
 out = {"envs": n, "bytes_per_env": 315, "source": "scripts/ubench/mover.hip via scripts/r05_mover_prof.sh", "cases": {}}
+if d == "-":
+    out = json.load(open(summary))
 for c, label in (("5", "12 waves per CU (the bulk step kernel's occupancy), no arithmetic"),
                  ("9", "12 waves per CU, 1 700 VALU per lane between the loads and the stores")):
+    if d == "-":
+        break
     durs = []
     for f in glob.glob(os.path.join(d, f"trace{c}", "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -38,20 +43,25 @@ for c, label in (("5", "12 waves per CU (the bulk step kernel's occupancy), no a
     stats = glob.glob(os.path.join(d, f"trace{c}", "**", "*kernel_stats.csv"), recursive=True)
     if stats and c == "5":
         shutil.copy(stats[0], os.path.join(root, "profiles", "r05_mover_4m_kernel_stats.csv"))
-# the event-timed sweep of the same binary (100 launches per hipGraph, profiles/r05_mover_sweep_4m.txt):
-# the launch period of the pattern, comparable with bench.py's per-step period
-sweep = os.path.join(root, "profiles", "r05_mover_sweep_4m.txt")
-if os.path.exists(sweep):
-    rows = []
+# the event-timed sweeps of the same binary (100 launches per hipGraph): the fastest launch period of
+# the pattern over every occupancy (waves per CU, by an LDS pad) and VALU count tried -- the ceiling
+# the step's own period is compared with (bench.py pattern_ceiling)
+rows = []
+for name in ("r05_mover_sweep_4m.txt", "r05_mover_occupancy_4m.txt"):
+    sweep = os.path.join(root, "profiles", name)
+    if not os.path.exists(sweep):
+        continue
     for ln in open(sweep):
-        if "waves/CU 12" in ln:
-            rows.append((int(ln.split("VALU/lane")[1].split(":")[0]), float(ln.split(":")[1].split("us")[0])))
-    if rows:
-        best = min(rows, key=lambda r: r[1])
-        out["period_us_event_timed"] = best[1]
-        out["period_source"] = (f"{sweep[len(root) + 1:]}: the fastest 12-waves-per-CU case ({best[0]} VALU per lane), "
-                                "HIP events over 100-launch graphs")
-        out["ceiling_GBs_315"] = 315 * n / best[1] / 1e3
-with open(os.path.join(root, "profiles", "r05_mover_4m_pmc_summary.json"), "w") as f:
+        if "waves/CU" in ln and "us/launch" in ln:
+            occ = ln.split("waves/CU")[1].split()[0]
+            rows.append((name, occ, int(ln.split("VALU/lane")[1].split(":")[0]), float(ln.split(":")[1].split("us")[0])))
+if rows:
+    best = min(rows, key=lambda r: r[3])
+    out["period_us_event_timed"] = best[3]
+    out["period_source"] = (f"profiles/{best[0]}: the fastest case of the sweeps ({best[1]} waves per CU, {best[2]} VALU "
+                            "per lane), HIP events over 100-launch graphs")
+    out["ceiling_GBs_315"] = 315 * n / best[3] / 1e3
+    out["sweep_cases"] = len(rows)
+with open(summary, "w") as f:
     json.dump(out, f, indent=1)
-print(json.dumps(out, indent=1))
+print(json.dumps({k: v for k, v in out.items() if k != "cases"}, indent=1))
