@@ -218,8 +218,9 @@ def pmc_summary(envs, dt, task, need="hbm_bytes_per_launch", tags=None):
 
 
 def pattern_ceiling():
-    """The committed measurement of the step kernel's own 4 M-env memory pattern with no arithmetic
-    (profiles/r05_mover_4m_pmc_summary.json, scripts/r05_mover_prof.sh), or None."""
+    """The committed measurement of the step kernel's own 4 M-env memory pattern (scripts/ubench/mover.hip:
+    the fastest launch period over its sweeps of occupancy and independent VALU load,
+    profiles/r05_mover_4m_pmc_summary.json, scripts/summarize_mover.py), or None."""
     path = os.path.join(ROOT, "profiles", "r05_mover_4m_pmc_summary.json")
     try:
         d = json.load(open(path))
