@@ -631,6 +631,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             if (a.fail_count) atomicAdd(a.fail_count, 1);
             if (a.out_status) a.out_status[job] = HG_E_TRIM;
         }
+        RSTAMP(61, "v"(l));   // the write-out issued
         lds_order();   // the next job's writes come after this job's reads
     }
 }

@@ -43,15 +43,17 @@ def main():
         while 4 + 4 * r < 62 and t[1 + 4 * r] > t[0] and t[4 + 4 * r] > t[1 + 4 * r]:
             rounds.append(((t[2 + 4 * r] - t[1 + 4 * r]), (t[3 + 4 * r] - t[2 + 4 * r]), (t[4 + 4 * r] - t[3 + 4 * r])))
             r += 1
-        rows.append(((t[63] - t[0]), (t[0] - t[62]) if t[62] > 0 and t[62] < t[0] else 0, rounds))
+        rows.append(((t[63] - t[0]), (t[0] - t[62]) if t[62] > 0 and t[62] < t[0] else 0, rounds,
+                     (t[61] - t[63]) if t[61] > t[63] else 0))
     env.close()
     if not rows:
         print("no trims stamped")
         return
     tot = np.array([r[0] for r in rows]) / ghz / 1e3
     st = np.array([r[1] for r in rows]) / ghz / 1e3
+    wr = np.array([r[3] for r in rows]) / ghz / 1e3
     print(f"{len(rows)} stamped trims ({mode}): total median {np.median(tot):.2f} us (p90 {np.percentile(tot, 90):.2f}), "
-          f"start-up median {np.median(st):.2f} us")
+          f"start-up median {np.median(st):.2f} us, write-out issue median {np.median(wr):.2f} us")
     for r in range(max(len(x[2]) for x in rows)):
         v = np.array([x[2][r] for x in rows if len(x[2]) > r]) / ghz / 1e3
         print(f"round {r}: n={len(v)}  eval {np.median(v[:, 0]):.2f}  accept+columns {np.median(v[:, 1]):.2f}  "
