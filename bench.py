@@ -593,8 +593,14 @@ def age(args, torch, env, bank, B, dt=None):
     if args.dry_run:
         return 0
     steps = int(round(args.age_seconds / (dt or args.dt)))
+    t_last = time.time()
     for k in range(steps):
         env.step_async(bank[k % B], with_reset_info=False)
+        if (k + 1) % 500 == 0:   # under a profiler each dispatch is slow: a line now and then shows progress
+            torch.cuda.synchronize()
+            if time.time() - t_last > 20:
+                progress(f"ageing: {k + 1} / {steps} steps")
+                t_last = time.time()
     torch.cuda.synchronize()
     return steps
 
