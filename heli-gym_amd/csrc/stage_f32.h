@@ -412,13 +412,22 @@ HD Kin kinematics(const X16& s, const Att2& at) {
 
 // The landing gear's loads added into the totals, only where some lane of the wave may touch
 // (`ran`: the wave took the branch).  QUIRK: the moment uses the ACCUMULATED force (:397).
+// ALWAYS (the lone-wave kernels, with the factored form's per-point selects): no wave-uniform skip.
+// In an aged population nearly every wave has a lane within the gear's reach of the ground, so the
+// skip is rarely taken, and without the branch the scheduler interleaves the gear with the rest of
+// the stage (65 536 envs: 7.07 -> 6.93 us).  Waves with no lane near the ground add zeros.  With
+// several waves per SIMD (the bulk variant) the skip stays: there the extra registers spill.
+#ifndef HG_GEAR_ALWAYS_LONE
+#define HG_GEAR_ALWAYS_LONE 1
+#endif
+template <bool ALWAYS = false>
 HD void gear_add(const Params<float>& P, const StepCtx& c, const X16& s, const Att2& at, float n2, float& Fx, f2& Fyz,
                  float& Mx, float& My, float& Mz, bool& ran) {
     const float z = s.wz.y, p = s.pq.x, q = s.pq.y, r = s.rt.x;
     const f2 SC0 = at.a[0];
     const float s1 = at.a[1].x, c1 = at.a[1].y;
 #if !defined(HG_ISA_HOT) && !defined(HG_ISA_NOGEAR)
-    if (wave_any(z > c.cz)) {
+    if ((ALWAYS && HG_GEAR_FACTORED == 3) || wave_any(z > c.cz)) {
 #else
     if (false) {
 #endif
@@ -542,19 +551,20 @@ struct StagePre {
     f2 Fl12;
 };
 
+template <bool ALWAYS = false>
 HD StagePre stage_pre(const Params<float>& P, const StepCtx& c, const X16& s, const Att2& at) {
     StagePre o;
     o.kin = kinematics(s, at);
     o.gear = false;
     // (-0 + x == x for every x, so the totals later add exactly what the inline form adds)
     o.Fl0 = -0.f; o.Fl12 = f2{-0.f, -0.f}; o.Ml0 = -0.f; o.Ml1 = -0.f; o.Ml2 = -0.f;
-    gear_add(P, c, s, at, o.kin.n2, o.Fl0, o.Fl12, o.Ml0, o.Ml1, o.Ml2, o.gear);
+    gear_add<ALWAYS>(P, c, s, at, o.kin.n2, o.Fl0, o.Fl12, o.Ml0, o.Ml1, o.Ml2, o.gear);
     return o;
 }
 
 // One evaluation of the model at stage state s (helicopter_dynamics.py:400-489) -> derivatives k;
 // with OBS also the 17 observations (:471-488) and the total power.
-template <bool OBS, bool PRE = false>
+template <bool OBS, bool PRE = false, bool ALWAYS = false>
 HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, const X16& s, const Att2& at, X16& k,
                   float* __restrict__ obs, const StagePre* pre = nullptr) {
 #ifdef HG_ISA_MARKS
@@ -681,7 +691,7 @@ HD void stage_f32(const Params<float>& P, const StepK& K, const StepCtx& c, cons
         }
     } else {
         bool ran = false;
-        gear_add(P, c, s, at, n2, Fx, Fyz, Mx, My, Mz, ran);
+        gear_add<ALWAYS>(P, c, s, at, n2, Fx, Fyz, Mx, My, Mz, ran);
     }
 
     // ---- equations of motion (:448-470)
@@ -775,6 +785,7 @@ HD Att2 att0(const float* hs) {
 // small-batch kernel runs it while its helper wave steps the wind), finish() the rest.
 template <bool LONE, bool PRE1 = false>
 struct RK4Step {
+    static constexpr bool kGearAlways = LONE && HG_GEAR_ALWAYS_LONE;
     X16 h;
     Att2 a0;
     StepK K;
@@ -788,7 +799,7 @@ struct RK4Step {
         h = to_x16(hs);
         a0 = a;
         K = k;
-        if constexpr (PRE1) pre1 = stage_pre(P, c, h, a0);
+        if constexpr (PRE1) pre1 = stage_pre<kGearAlways>(P, c, h, a0);
     }
     HD void finish(const Params<float>& P, const StepCtx& c, float* __restrict__ hs, float* __restrict__ d,
                    float* __restrict__ obs);
@@ -798,16 +809,16 @@ template <bool LONE, bool PRE1>
 HD void RK4Step<LONE, PRE1>::finish(const Params<float>& P, const StepCtx& c, float* __restrict__ hs,
                                    float* __restrict__ d, float* __restrict__ obs) {
     X16 k, acc, st;
-    stage_f32<false, PRE1>(P, K, c, h, a0, k, obs, &pre1);
+    stage_f32<false, PRE1, kGearAlways>(P, K, c, h, a0, k, obs, &pre1);
     HG_STAGE_STAMP(5, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<true>(h, k, acc, st, P.half_dt);
-    stage_f32<false>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     HG_STAGE_STAMP(6, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<false>(h, k, acc, st, P.half_dt);
-    stage_f32<false>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     HG_STAGE_STAMP(7, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<false>(h, k, acc, st, P.dt);
-    stage_f32<true>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<true, false, kGearAlways>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     rk_update2(h, k, acc, P.dt6);
     from_x16(h, hs);
     // (the rotor azimuths hs[2], hs[3] are not stepped here: see az_advance)
