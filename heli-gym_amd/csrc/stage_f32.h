@@ -295,6 +295,7 @@ HD StepCtx step_ctx(const Params<float>& P, float a0, float a1, float a2, float 
 // within 0.55 fp32 ulp of sin / cos over that range evaluated in fp32 (the round-4 short series: 1.19
 // ulp at 0.05), so every wave up to 0.25 rad (all but ~1 % of an aged population's waves) takes this
 // one branch-free form; past it the wave takes the full sincos.
+template <bool MIDALL = false>   // (no long-series branch to remove here)
 HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
     const f2 d01 = pp - pp0;   // phi, psi increments
     const float d2 = th - th0;
@@ -325,6 +326,9 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
     return a;
 }
 #else
+// MIDALL (A/B): the long series formed by every wave and selected per lane, no wave-uniform branch
+// around it (the full sincos keeps its branch)
+template <bool MIDALL = false>
 HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
     const f2 d01 = pp - pp0;   // phi, psi increments
     const float d2 = th - th0;
@@ -346,7 +350,7 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
     // 6e-11 at 0.25 rad, so a few fp32 ulps like the short series at 0.05), past it the full sincos
     const bool small = m_fabs(d01.x) <= 0.05f && m_fabs(d01.y) <= 0.05f && m_fabs(d2) <= 0.05f;
 #ifndef HG_ISA_HOT   // (analysis builds only: the hot path without its cold branches)
-    if (wave_any(!small)) {
+    if ((MIDALL && HG_MID_ANGLE_MRAD > 0) || wave_any(!small)) {
 #else
     if (false) {
 #endif
@@ -354,14 +358,18 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
 #if HG_MID_ANGLE_MRAD > 0
         constexpr float kMid = HG_MID_ANGLE_MRAD * 1e-3f;   // (NaN increments: neither, the full sincos)
         const bool mid = m_fabs(d01.x) <= kMid && m_fabs(d01.y) <= kMid && m_fabs(d2) <= kMid;
-        if (!small && mid) {
+        if (MIDALL || (!small && mid)) {
             const f2 ms = d01 + (d01 * q01) * (K.c6 + q01 * (1.f / 120.f + q01 * (-1.f / 5040.f)));
             const f2 mc = 1.f + q01 * (-0.5f + q01 * (K.c24 + q01 * (-1.f / 720.f + q01 * (1.f / 40320.f))));
             const float ms2 = d2 + (d2 * q2) * (K.c6.x + q2 * (1.f / 120.f + q2 * (-1.f / 5040.f)));
             const float mc2 = 1.f + q2 * (-0.5f + q2 * (K.c24.x + q2 * (-1.f / 720.f + q2 * (1.f / 40320.f))));
-            a.a[0] = fma_swn_bx(A0, ms, A0 * mc.x);
-            a.a[1] = A1 * mc2 + f2{A1.y, -A1.x} * ms2;
-            a.a[2] = fma_swn_by(A2, ms, A2 * mc.y);
+            const f2 m0 = fma_swn_bx(A0, ms, A0 * mc.x);
+            const f2 m1 = A1 * mc2 + f2{A1.y, -A1.x} * ms2;
+            const f2 m2 = fma_swn_by(A2, ms, A2 * mc.y);
+            const bool take = MIDALL ? (!small && mid) : true;
+            a.a[0] = take ? m0 : a.a[0];
+            a.a[1] = take ? m1 : a.a[1];
+            a.a[2] = take ? m2 : a.a[2];
         }
         if (wave_any(!mid)) {
             HG_STAGE_FLAG(8);
@@ -419,6 +427,12 @@ HD Kin kinematics(const X16& s, const Att2& at) {
 // several waves per SIMD (the bulk variant) the skip stays: there the extra registers spill.
 #ifndef HG_GEAR_ALWAYS_LONE
 #define HG_GEAR_ALWAYS_LONE 1
+#endif
+// The attitude long series without its branch (att_step<true>): in the small-batch helper kernel
+// (4 096 envs 5.27 -> 5.21 us); in the other lone-wave kernels it costs more than the branch
+// (65 536 envs 6.94 -> 7.06 us; profiles/r05_gear_always_ab.txt)
+#ifndef HG_MIDALL_HELP
+#define HG_MIDALL_HELP 1
 #endif
 template <bool ALWAYS = false>
 HD void gear_add(const Params<float>& P, const StepCtx& c, const X16& s, const Att2& at, float n2, float& Fx, f2& Fyz,
@@ -786,6 +800,7 @@ HD Att2 att0(const float* hs) {
 template <bool LONE, bool PRE1 = false>
 struct RK4Step {
     static constexpr bool kGearAlways = LONE && HG_GEAR_ALWAYS_LONE;
+    static constexpr bool kMidAll = LONE && PRE1 && HG_MIDALL_HELP;   // PRE1: the helper kernel
     X16 h;
     Att2 a0;
     StepK K;
@@ -812,13 +827,13 @@ HD void RK4Step<LONE, PRE1>::finish(const Params<float>& P, const StepCtx& c, fl
     stage_f32<false, PRE1, kGearAlways>(P, K, c, h, a0, k, obs, &pre1);
     HG_STAGE_STAMP(5, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<true>(h, k, acc, st, P.half_dt);
-    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step<kMidAll>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     HG_STAGE_STAMP(6, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<false>(h, k, acc, st, P.half_dt);
-    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step<kMidAll>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     HG_STAGE_STAMP(7, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<false>(h, k, acc, st, P.dt);
-    stage_f32<true, false, kGearAlways>(P, K, c, st, att_step(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<true, false, kGearAlways>(P, K, c, st, att_step<kMidAll>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     rk_update2(h, k, acc, P.dt6);
     from_x16(h, hs);
     // (the rotor azimuths hs[2], hs[3] are not stepped here: see az_advance)
