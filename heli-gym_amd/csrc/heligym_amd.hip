@@ -431,7 +431,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
             ws[0] = g2.z; ws[1] = g2.w; ws[2] = g3.x; ws[3] = g3.y; ws[4] = g3.z;
             HSTAMP(2, "v"(g0.w), "v"(g1.x));
             draw_eta<false>(a, seed_p, envoff_p, PH, 0, blk0, lo, __float_as_int(g0.w), __float_as_int(g1.x), eta);
-            hg::wind_step_f32(PH, ws, carry, eta, W);
+            hg::wind_step_f32<true>(PH, ws, carry, eta, W);
             HSTAMP(3, "v"(W[0]), "v"(ws[4]));
             float* sw = s_wind + wv * 8 * 64 + lane;
             sw[0] = W[0]; sw[64] = W[1]; sw[128] = W[2];
@@ -522,7 +522,7 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
 
     // ground height under the committed position (F6), wind step (Heli.step :195-199)
     TSTAMP(2, "v"(eta[2]), "v"(eta[0]));
-    hg::wind_step_f32(P, ws, carry, eta, W);
+    hg::wind_step_f32<NT>(P, ws, carry, eta, W);   // (the lone-wave kernels: the uniform-branch form)
     TSTAMP(3, "v"(W[2]), "v"(W[0]));
     const hg::Ground<float> h_c = hg::ground_combine<float>(tex_c, cell_c);
 
@@ -708,7 +708,19 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
             obs[c] = do_reset ? v : obs[c];
         }
     }
-    if (do_reset) {
+    if constexpr (NT) {
+        // the lone-wave kernels: the same assignments as selects, no divergent branch (65 536 envs
+        // -0.08 us; the bulk variant keeps the branch)
+#pragma unroll
+        for (int c = 0; c < 5; ++c) ws[c] = do_reset ? 0.f : ws[c];
+        carry[0] = do_reset ? carry[0] : obs[4];
+        carry[1] = do_reset ? carry[1] : obs[5];
+        carry[2] = do_reset ? carry[2] : obs[6];
+        carry[3] = do_reset ? carry[3] : obs[16];
+        step = do_reset ? 0 : ((FEAT && P.autoreset_next && done) ? -step - 1 : step);
+        succ = do_reset ? 0 : succ;
+        epi = do_reset ? epi + 1 : epi;
+    } else if (do_reset) {
 #pragma unroll
         for (int c = 0; c < 5; ++c) ws[c] = 0.f;
         step = 0;

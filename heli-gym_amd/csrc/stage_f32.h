@@ -204,8 +204,9 @@ HD StepK step_k(const Params<float>& P) {
 // Q = (vs0, ws0), R = (vs1, ws1); u is the first-order filter.  QUIRK: the update is
 // s += dt k4, the stage inputs still formed from k1..k3; the wind output from the stage-4 input.
 // Same operations per component as physics.h wind_step, so the same roundings.
+template <bool UNIFORM = false>
 HD void wind_step_f32(const Params<float>& P, float s[5], const float carry[4], const float eta[3], float W[3]) {
-    const WindPar<float> w = wind_params(P, carry);
+    const WindPar<float> w = wind_params<float, UNIFORM>(P, carry);
     const f2 A = f2{w.a_v, w.a_w}, B = f2{w.b_v, w.b_w}, E = f2{eta[1], eta[2]};
     const float U = s[0];
     const f2 Q = f2{s[1], s[3]}, R = f2{s[2], s[4]};
