@@ -296,7 +296,7 @@ HD StepCtx step_ctx(const Params<float>& P, float a0, float a1, float a2, float 
 // within 0.55 fp32 ulp of sin / cos over that range evaluated in fp32 (the round-4 short series: 1.19
 // ulp at 0.05), so every wave up to 0.25 rad (all but ~1 % of an aged population's waves) takes this
 // one branch-free form; past it the wave takes the full sincos.
-template <bool MIDALL = false>   // (no long-series branch to remove here)
+template <bool MIDALL = false, bool SEL = false>   // (no long-series branch to remove here)
 HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
     const f2 d01 = pp - pp0;   // phi, psi increments
     const float d2 = th - th0;
@@ -327,9 +327,10 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
     return a;
 }
 #else
-// MIDALL (A/B): the long series formed by every wave and selected per lane, no wave-uniform branch
-// around it (the full sincos keeps its branch)
-template <bool MIDALL = false>
+// MIDALL: the long series formed by every wave and selected per lane, no wave-uniform branch around
+// it.  SEL: inside the wave-uniform branches, the per-lane choices as selects instead of divergent
+// branches (every lane runs the series / sincos, as a divergent branch's masked lanes would).
+template <bool MIDALL = false, bool SEL = false>
 HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float th) {
     const f2 d01 = pp - pp0;   // phi, psi increments
     const float d2 = th - th0;
@@ -359,7 +360,7 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
 #if HG_MID_ANGLE_MRAD > 0
         constexpr float kMid = HG_MID_ANGLE_MRAD * 1e-3f;   // (NaN increments: neither, the full sincos)
         const bool mid = m_fabs(d01.x) <= kMid && m_fabs(d01.y) <= kMid && m_fabs(d2) <= kMid;
-        if (MIDALL || (!small && mid)) {
+        if (MIDALL || SEL || (!small && mid)) {
             const f2 ms = d01 + (d01 * q01) * (K.c6 + q01 * (1.f / 120.f + q01 * (-1.f / 5040.f)));
             const f2 mc = 1.f + q01 * (-0.5f + q01 * (K.c24 + q01 * (-1.f / 720.f + q01 * (1.f / 40320.f))));
             const float ms2 = d2 + (d2 * q2) * (K.c6.x + q2 * (1.f / 120.f + q2 * (-1.f / 5040.f)));
@@ -367,14 +368,19 @@ HD Att2 att_step(const StepK& K, const Att2& a0, f2 pp0, float th0, f2 pp, float
             const f2 m0 = fma_swn_bx(A0, ms, A0 * mc.x);
             const f2 m1 = A1 * mc2 + f2{A1.y, -A1.x} * ms2;
             const f2 m2 = fma_swn_by(A2, ms, A2 * mc.y);
-            const bool take = MIDALL ? (!small && mid) : true;
+            const bool take = (MIDALL || SEL) ? (!small && mid) : true;
             a.a[0] = take ? m0 : a.a[0];
             a.a[1] = take ? m1 : a.a[1];
             a.a[2] = take ? m2 : a.a[2];
         }
         if (wave_any(!mid)) {
             HG_STAGE_FLAG(8);
-            if (!mid) {
+            if constexpr (SEL) {
+                const f2 f0 = sincos2(pp.x), f1 = sincos2(th), f2s = sincos2(pp.y);
+                a.a[0] = mid ? a.a[0] : f0;
+                a.a[1] = mid ? a.a[1] : f1;
+                a.a[2] = mid ? a.a[2] : f2s;
+            } else if (!mid) {
                 a.a[0] = sincos2(pp.x);
                 a.a[1] = sincos2(th);
                 a.a[2] = sincos2(pp.y);
@@ -434,6 +440,11 @@ HD Kin kinematics(const X16& s, const Att2& at) {
 // (65 536 envs 6.94 -> 7.06 us; profiles/r05_gear_always_ab.txt)
 #ifndef HG_MIDALL_HELP
 #define HG_MIDALL_HELP 1
+#endif
+// The per-lane attitude choices inside its wave-uniform branches as selects, in the lone-wave kernels
+// other than the helper one (65 536 envs 6.83 -> 6.79 us; 4 096 envs, the helper kernel, +0.03 us)
+#ifndef HG_ATT_SEL_LONE
+#define HG_ATT_SEL_LONE 1
 #endif
 template <bool ALWAYS = false>
 HD void gear_add(const Params<float>& P, const StepCtx& c, const X16& s, const Att2& at, float n2, float& Fx, f2& Fyz,
@@ -802,6 +813,7 @@ template <bool LONE, bool PRE1 = false>
 struct RK4Step {
     static constexpr bool kGearAlways = LONE && HG_GEAR_ALWAYS_LONE;
     static constexpr bool kMidAll = LONE && PRE1 && HG_MIDALL_HELP;   // PRE1: the helper kernel
+    static constexpr bool kAttSel = LONE && !PRE1 && HG_ATT_SEL_LONE;   // (not the helper kernel)
     X16 h;
     Att2 a0;
     StepK K;
@@ -828,13 +840,13 @@ HD void RK4Step<LONE, PRE1>::finish(const Params<float>& P, const StepCtx& c, fl
     stage_f32<false, PRE1, kGearAlways>(P, K, c, h, a0, k, obs, &pre1);
     HG_STAGE_STAMP(5, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<true>(h, k, acc, st, P.half_dt);
-    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step<kMidAll>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step<kMidAll, kAttSel>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     HG_STAGE_STAMP(6, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<false>(h, k, acc, st, P.half_dt);
-    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step<kMidAll>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<false, false, kGearAlways>(P, K, c, st, att_step<kMidAll, kAttSel>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     HG_STAGE_STAMP(7, "v"(k.uv.x), "v"(k.pq.y));
     rk_stage2<false>(h, k, acc, st, P.dt);
-    stage_f32<true, false, kGearAlways>(P, K, c, st, att_step<kMidAll>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
+    stage_f32<true, false, kGearAlways>(P, K, c, st, att_step<kMidAll, kAttSel>(K, a0, h.pp, h.rt.y, st.pp, st.rt.y), k, obs);
     rk_update2(h, k, acc, P.dt6);
     from_x16(h, hs);
     // (the rotor azimuths hs[2], hs[3] are not stepped here: see az_advance)
