@@ -1017,7 +1017,8 @@ def main():
                     "note": "reset_mode='retrim': each auto-reset re-trimmed on the device (Newton trim against the "
                             "env's last wind, the reference's reset from episode 2 on), hipGraph"
                             + ("; next-step auto-reset (make_vec's configuration): the episodes a step ends are "
-                               "trimmed on side streams while the next step runs" if ov else "")}
+                               "trimmed in the first blocks of the next step's launch (step_ov_kernel)"
+                               if ov else "")}
                 envr.close()
 
         if world == 1 and not args.no_secondary and not args.dry_run and args.envs < OUT_OF_CACHE_ENVS:
