@@ -162,6 +162,9 @@ constexpr int kTplFloats = (int)(sizeof(Template<float>) / sizeof(float));
 static_assert(kTplFloats <= 64, "reset template must fit one float per lane");
 // the template's device copy holds one float per lane of a wave (HG_TPL_FULL: every lane loads one)
 constexpr size_t kTplAlloc = 64 * sizeof(float);
+#ifndef HG_RT_QUEUE_LATE   // the re-trim queue's records written after the state stores (lone-wave kernels)
+#define HG_RT_QUEUE_LATE 1
+#endif
 #ifndef HG_TPL_FULL_HELP
 #define HG_TPL_FULL_HELP 1
 #endif
@@ -489,6 +492,33 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     }
     const int nsteps = MULTI ? a.nsteps : 1;
     bool defer_st = false;   // (one step per launch) a deferred reset: the step counter alone is stored
+    // the re-trim queue (below): the wave's job mask, the slot counter's old value (leader lane), this
+    // lane's job and its trim wind
+    unsigned long long rt_mask = 0;
+    int rt_base = 0;
+    bool rt_job = false, rt_next = false;
+    // (the bulk variant writes them at once: the values kept live past the stores cost it registers,
+    // 262 144 envs 46.6 -> 47.3 us with the late write)
+    constexpr bool kRtLate = HG_RT_QUEUE_LATE && NT && !MULTI;
+    unsigned long long rc_mask = 0;   // the same for the compacted reset info
+    int rc_base = 0;
+    bool rc_job = false;
+    float fo[kRtLate ? 17 : 1];
+    float rw0 = 0.f, rw1 = 0.f, rw2 = 0.f;
+    auto rt_queue = [&]() {
+        if (FEAT && rt_mask) {
+            const int leader = __ffsll((long long)rt_mask) - 1;
+            const int slot = __builtin_amdgcn_readlane(rt_base, leader) + __popcll(rt_mask & ((1ull << lane) - 1ull));
+            if (rt_job && slot < n) {
+                if (rt_next) {   // a next-step reset: the wind recorded at the episode's last step
+                    rw0 = a.retrim_wind[i];
+                    rw1 = a.retrim_wind[n + i];
+                    rw2 = a.retrim_wind[2 * n + i];
+                }
+                a.retrim_recs[slot] = make_int4((int32_t)i, __float_as_int(rw0), __float_as_int(rw1), __float_as_int(rw2));
+            }
+        }
+    };
     for (int sstep = 0; sstep < nsteps; ++sstep) {
     // MULTI: the constants are re-read (scalar cache) each step rather than kept live across the
     // loop, where ~130 of them would spill out of the SGPR file
@@ -631,10 +661,21 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
         }
     }
 
-    // compacted reset info with a wave-ballot compaction
+    // compacted reset info with a wave-ballot compaction (HG_RT_QUEUE_LATE: as the re-trim queue
+    // below, the slots used after the state stores, the terminal observations kept until then)
     if (FEAT && P.autoreset && a.reset_count) {
+        if constexpr (kRtLate) asm volatile("" ::"v"(tpl));
         const unsigned long long mask = __ballot(do_reset);
-        if (mask) {
+        if constexpr (kRtLate) {
+            rc_mask = mask;
+            if (mask) {
+                const int leader = __ffsll((long long)mask) - 1;
+                if (lane == leader) rc_base = atomicAdd(a.reset_count, __popcll(mask));
+            }
+#pragma unroll
+            for (int c = 0; c < 17; ++c) fo[c] = obs[c];
+            rc_job = do_reset;
+        } else if (mask) {
             const int leader = __ffsll((long long)mask) - 1;
             int base = 0;
             if (lane == leader) base = atomicAdd(a.reset_count, __popcll(mask));
@@ -662,27 +703,25 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
                 a.ov_recs[slot] = make_int4((int32_t)i, __float_as_int(W[0]), __float_as_int(W[1]), __float_as_int(W[2]));
         }
     }
-    if (FEAT && P.reset_retrim) {   // queue the resets for retrim_kernel (which overwrites the template)
-        const unsigned long long mask = __ballot(do_reset && !defer);
-        if (mask) {
-            const int leader = __ffsll((long long)mask) - 1;
-            int base = 0;
-            if (lane == leader) base = atomicAdd(a.retrim_count + (a.retrim_slot > 0 ? a.retrim_slot : 0), __popcll(mask));
-            base = __shfl(base, leader);
-            const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
-            if (do_reset && !defer && slot < n) {
-                // the job carries its trim wind: this step's (same-step reset), or the one recorded at
-                // the episode's last step (next-step reset)
-                float w0 = W[0], w1 = W[1], w2 = W[2];
-                if (P.autoreset_next) {
-                    w0 = a.retrim_wind[i];
-                    w1 = a.retrim_wind[n + i];
-                    w2 = a.retrim_wind[2 * n + i];
-                }
-                a.retrim_recs[slot] = make_int4((int32_t)i, __float_as_int(w0), __float_as_int(w1), __float_as_int(w2));
-            }
+    // queue the resets for retrim_kernel (which overwrites the template).  HG_RT_QUEUE_LATE: the slot
+    // counter's atomic is issued here and its value used after the state stores (lone-wave
+    // kernels, one step per launch: 65 536 envs same-step re-trim 30.43 -> 30.11 us), so that the round trip of the device-scope atomic overlaps them instead of lengthening
+    // the wave (the library is built without the atomic optimizer, which would read the value here)
+    if (FEAT && P.reset_retrim) {
+        // the reset template's load (issued at the start) waited for here, not after the atomic
+        if constexpr (kRtLate) asm volatile("" ::"v"(tpl));
+        rt_job = do_reset && !defer;
+        rt_mask = __ballot(rt_job);
+        if (rt_mask) {
+            const int leader = __ffsll((long long)rt_mask) - 1;
+            if (lane == leader) rt_base = atomicAdd(a.retrim_count + (a.retrim_slot > 0 ? a.retrim_slot : 0), __popcll(rt_mask));
         }
+        rt_next = P.autoreset_next;
+        rw0 = W[0];   // the job's trim wind (same-step reset; a next-step reset reads its own, below)
+        rw1 = W[1];
+        rw2 = W[2];
     }
+    if (!kRtLate) rt_queue();
     if (FEAT && P.env_templates) {   // this env's own reset target (its own trim condition)
         if (do_reset) {
             const float* tr = a.tmpl_env + (int64_t)i * kTplFloats;
@@ -692,6 +731,9 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
             for (int c = 0; c < 4; ++c) carry[c] = tr[18 + c];
 #pragma unroll
             for (int c = 0; c < 17; ++c) obs[c] = tr[22 + c];
+            // the loads complete inside this branch (vmcnt(0)): the memory-counter waits after the join
+            // then need not count the re-trim queue's atomic on the other path
+            if constexpr (kRtLate) __builtin_amdgcn_s_waitcnt(0xF70);
         }
     } else if (__ballot(do_reset)) {
 #if HG_TIMING
@@ -764,6 +806,20 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
         st_lane<kNTS>(GRP(st_b, 6), t, f32x4{hs[10], hs[11], hs[12], hs[13]});
     }
 #undef GRP
+    if (kRtLate) rt_queue();
+    if constexpr (kRtLate) {
+        if (FEAT && rc_mask) {
+            const int leader = __ffsll((long long)rc_mask) - 1;
+            const int slot = __builtin_amdgcn_readlane(rc_base, leader) + __popcll(rc_mask & ((1ull << lane) - 1ull));
+            if (rc_job && slot < n) {
+                if (a.reset_index) a.reset_index[slot] = (int32_t)i;
+                if (a.final_obs) {
+#pragma unroll
+                    for (int c = 0; c < 17; ++c) a.final_obs[(int64_t)slot * 17 + c] = fo[c];
+                }
+            }
+        }
+    }
 
     TSTAMP(11, "v"(tid));
 #if HG_TIMING

@@ -24,7 +24,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize",
          "-ffp-contract=on", "-Wno-unused-result",
-         "-mllvm", "-amdgpu-kernarg-preload-count=6", "-mllvm", "-disable-vector-combine"]
+         "-mllvm", "-amdgpu-kernarg-preload-count=6", "-mllvm", "-disable-vector-combine",
+         "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
 PARAMS_BYTES_MAX = 4096
 
 
