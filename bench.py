@@ -916,7 +916,7 @@ def main():
 
         if not args.no_secondary and not args.dry_run:
             # the same step with the compacted reset info (same-step auto-reset: reset indices and
-            # terminal observations compacted in-kernel; captured, so a memset node zeroes the count)
+            # terminal observations compacted in-kernel; each step's kernel zeroes a later step's count)
             if args.reset_mode == "template" and args.autoreset_mode == "same_step":
                 progress("step_with_reset_info / step_api_eager")
 
@@ -929,7 +929,8 @@ def main():
                     "value": total_envs * K / s_ri, "unit": "env-steps/s", "ms_per_step": s_ri / K * 1e3,
                     "resets_in_window": rs_ri,
                     "note": "step_async(with_reset_info=True): reset_index + final_obs compaction "
-                            "(hg_step_chained; a memset node per captured step), hipGraph"}
+                            "(hg_step_chained: the counts rotate over three slots, each step's kernel zeroing a later one's; "
+                            "no zeroing launch), hipGraph"}
                 # HeliVecEnv.step() as an RL loop calls it: eager, lazy info
                 Ke = 200   # (its own window length: 20 eager launches would carry the HIP events' latency)
 
