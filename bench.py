@@ -425,7 +425,7 @@ def progress(msg):
 
 
 class TimedGraph:
-    """One hipGraph per window: a pre-roll of B steps, the episode count, a GPU clock stamp, exactly K
+    """One hipGraph per window: a pre-roll of P = max(B, 1 000) steps (HG_TG_PREROLL), the episode count, a GPU clock stamp, exactly K
     steps, a second stamp, the episode count again.  The stamps (hg_clock_stamp: the constant 100 MHz
     clock, written by a one-lane kernel) bracket the K timed steps, so a window of any K measures them
     in steady state: the GPU is already stepping when the first stamp is taken, and the window holds K
@@ -466,7 +466,7 @@ class TimedGraph:
         # a pre-roll of 1 000 steps instead of 100: 8.17 -> 7.89 us (the GPU's clock and caches settle)
         layout = int(os.environ.get("HG_TG_LAYOUT", "2"))
         W = self.W = 8 if layout == 2 else 0
-        P = int(os.environ.get("HG_TG_PREROLL", str(max(B, 1000))))
+        P = self.P = int(os.environ.get("HG_TG_PREROLL", str(max(B, 1000))))
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=s):
             for k in range(P - W):
@@ -504,8 +504,8 @@ def windows(torch, dev, one_step, K, B, env=None):
     if os.environ.get("HG_BENCH_OUTER_WINDOWS") != "1" and env is not None and hasattr(env, "lib"):
         try:
             tg = TimedGraph(torch, dev, one_step, K, B, env)
-            return tg, (tg,), (f"one hipGraph per window: {B} pre-roll steps, then the {K} timed steps between "
-                               "two GPU clock stamps")
+            return tg, (tg,), (f"one hipGraph per window: {tg.P} pre-roll steps (the last {tg.W} after the first "
+                               f"episode count), then the {K} timed steps between two GPU clock stamps")
         except Exception as exc:   # (reported in the mode string)
             torch.cuda.synchronize()
             progress(f"TimedGraph unavailable ({exc}); graph replays")
@@ -825,8 +825,11 @@ def main():
         # refuses two ranks on one device); timings from such a run are not a measurement
         backend = os.environ.get("HG_BENCH_BACKEND", "nccl")
         if backend == "nccl":
+            # the device is selected after the rendezvous: while rank 0's config-5 child measures, the
+            # ranks waiting here hold no HIP context on the GPUs the child's ranks use (the
+            # communicators are created lazily, at the first collective, on the device set here)
+            dist.init_process_group("nccl", timeout=pg_timeout)
             torch.cuda.set_device(local)
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"), timeout=pg_timeout)
         else:
             torch.cuda.set_device(local % torch.cuda.device_count())
             dist.init_process_group(backend, timeout=pg_timeout)

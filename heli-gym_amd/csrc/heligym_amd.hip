@@ -336,7 +336,9 @@ __device__ unsigned long long g_timing[HG_TIMING_WAVES][HG_TIMING_SLOTS];
         if ((tid & 63) == 0 && w_ < HG_TIMING_WAVES) g_timing[w_][j] = t_;                      \
     } while (0)
 // the stamping wave's tile from the hardware ids (the small-batch kernel's blocks are a stepping wave and
-// its helper: the stepping wave is wave 0, its tile the block)
+// its helper: the stepping wave is wave 0, its tile the block).  A 128-thread block is taken for the
+// small-batch kernel's, so the timing build keeps the one-wave step blocks of the default build.
+static_assert(HG_STEP_BLOCK != 128, "HG_TIMING builds tell the helper kernel's blocks by their 128 threads");
 #define HG_STAMP_WAVE() (blockDim.x == 128 ? (int)blockIdx.x : (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6))
 // the same stamp from inside the RK driver (stage_f32.h), where only the hardware ids are in scope
 #define HG_STAGE_STAMP(j, ...)                                                                  \
@@ -1195,6 +1197,10 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
     const double loc[3][3] = {{-(a.lg_FS_N - a.FS_CG), 0.0, -(a.lg_WL - a.WL_CG)},
                               {-(a.lg_FS_MN - a.FS_CG), a.lg_BL_MN, -(a.lg_WL - a.WL_CG)},
                               {-(a.lg_FS_MN - a.FS_CG), -a.lg_BL_MN, -(a.lg_WL - a.WL_CG)}};
+    // The lone-wave kernels' gear (stage_f32.h gear_add, HG_GEAR_FACTORED 3) reads only lg_loc[0][0],
+    // [1][0], [1][1] and [0][2]: it relies on this layout -- the nose wheel on the centre line, the
+    // mains mirrored about it, all three on one waterline -- which the reference's geometry always
+    // has (helicopter_dynamics.py:123-126).  hg_create checks it (gear_layout_ok) before any step.
     for (int g = 0; g < 3; ++g)
         for (int j = 0; j < 3; ++j) P.lg_loc[g][j] = (R)(loc[g][j] / 12.0);   // :123-126
     double reach = 0;
@@ -1285,6 +1291,7 @@ Params<R> derive(const hg_config& c, int rows, int cols) {
 hg::TrimSetup trim_setup(const Params<double>& P, const float2* hmap, const hg_trim_cond& tc) {
     hg::TrimSetup t;
     memset(&t, 0, sizeof(t));
+    t.piv[0][0] = -1;   // no pivot order (build_template records the env condition's)
     t.base[14] = (float)tc.yaw;
     t.base[2] = (float)tc.psi_mr;
     t.base[3] = (float)tc.psi_tr;
@@ -1303,15 +1310,18 @@ hg::TrimSetup trim_setup(const Params<double>& P, const float2* hmap, const hg_t
 
 // HelicopterDynamics.trim (helicopter_dynamics.py:491-555), serial: fp64 Newton with a central-
 // difference Jacobian and step halving, the reference's iteration logic.
+// piv_rec (4 x 16, optional): the pivot order of each of the first four Newton solves (hg::TrimSetup::piv;
+// the later entries repeat the last solve's, and stay untouched when the trim took no Newton step).
 int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond& tc, const double W[3],
-                hg_trim_result* out, double* jac_rec = nullptr, int32_t jac_max = 0, int32_t* jac_n = nullptr) {
+                hg_trim_result* out, double* jac_rec = nullptr, int32_t jac_max = 0, int32_t* jac_n = nullptr,
+                int8_t* piv_rec = nullptr) {
     const hg::TrimSetup T = trim_setup(P, hmap, tc);
     const double eps = hg::kTrimEps;
     double x[16], y[16];
     memcpy(x, T.x0, sizeof(x));
     hg::trim_fcn(P, T, x, W, y, nullptr, nullptr, nullptr);
     double tol = hg::trim_residual(y, T.yt);
-    int it = 0;
+    int it = 0, nsolve = 0;
     while (tol > eps) {
         double J[16][16], yp[16], ym[16], xp[16], xm[16], r[16], dir[16];
         for (int i = 0; i < 16; ++i) {
@@ -1328,7 +1338,11 @@ int32_t do_trim(const Params<double>& P, const float2* hmap, const hg_trim_cond&
             ++*jac_n;
         }
         for (int k = 0; k < 16; ++k) r[k] = y[k] - T.yt[k];
-        if (!hg::solve16(J, r, dir)) return fail(HG_E_TRIM, "trim: singular Jacobian");
+        int8_t piv[16];
+        if (!hg::solve16(J, r, dir, piv)) return fail(HG_E_TRIM, "trim: singular Jacobian");
+        if (piv_rec)
+            for (int k = nsolve; k < 4; ++k) memcpy(piv_rec + 16 * k, piv, 16);   // later steps: this order
+        ++nsolve;
         double step = 1.0, xn[16], yn[16], tn = 0;
         int j;
         for (j = 0; j < hg::kTrimLineSearch; ++j) {
@@ -1408,7 +1422,8 @@ struct hg_env {
     float* retrim_wind = nullptr;           // reset_mode RETRIM work buffers
     int32_t* retrim_list = nullptr;         // hg_reset's masked envs (their winds by env)
     int4* retrim_recs = nullptr;            // a step's auto-reset jobs {env, wind}
-    int32_t* retrim_count = nullptr;        // [0] jobs of hg_reset's re-trim, [1] failures so far, [2] invalid jobs
+    int32_t* retrim_count = nullptr;        // [0] jobs of hg_reset's re-trim, [1] failures so far, [2] invalid jobs,
+                                            // [3] solves tried with the given pivot order, [4] of them rejected
     int32_t* retrim_ring = nullptr;         // [3] jobs of a step's re-trim: step k counts into [k % 3] and
     uint64_t retrim_gen = 0;                //     zeroes [(k + 1) % 3] from its kernel (no memset launch)
     uint64_t retrim_chain = kChainBroken;   // chain key of the previous re-trim step (see chain_key)
@@ -1458,6 +1473,13 @@ struct DevGuard {
     }
 };
 
+// The gear layout the lone-wave kernels' factored gear relies on (derive(), stage_f32.h gear_add):
+// nose wheel on the centre line, mains mirrored about it, one waterline.
+static bool gear_layout_ok(const Params<float>& P) {
+    return P.lg_loc[0][1] == 0.f && P.lg_loc[2][0] == P.lg_loc[1][0] && P.lg_loc[2][1] == -P.lg_loc[1][1] &&
+           P.lg_loc[1][2] == P.lg_loc[0][2] && P.lg_loc[2][2] == P.lg_loc[0][2];
+}
+
 // Model constants after a configuration change (create and the setters).
 static void rederive(hg_env* e) {
     e->Pd = derive<double>(e->cfg, e->rows, e->cols);
@@ -1498,7 +1520,9 @@ static int32_t build_template(hg_env* e) {
     const double W[3] = {e->Pd.wm[0], e->Pd.wm[1], e->Pd.wm[2]};   // helicopter.py:55 (mean wind)
     hg_trim_result r;
     memset(&r, 0, sizeof(r));
-    const int32_t rc = do_trim(e->Pd, e->hmap_host.data(), e->cfg.trim, W, &r);
+    int8_t piv[4][16];
+    memset(piv, -1, sizeof(piv));
+    const int32_t rc = do_trim(e->Pd, e->hmap_host.data(), e->cfg.trim, W, &r, nullptr, 0, nullptr, &piv[0][0]);
     if (rc != HG_OK) return rc;
     e->trim = r;
     for (int c = 0; c < 18; ++c) e->tmpl.heli[c] = (float)r.state[c];
@@ -1508,6 +1532,7 @@ static int32_t build_template(hg_env* e) {
     e->tmpl.carry[2] = (float)r.obs[6];
     e->tmpl.carry[3] = (float)r.obs[16];
     e->setup = trim_setup(e->Pd, e->hmap_host.data(), e->cfg.trim);
+    memcpy(e->setup.piv, piv, sizeof(piv));   // the device trim's first-choice pivot order
     if (e->tmpl_dev) {   // device copies read by the step / re-trim kernels (after all queued work)
         hipError_t err = hipDeviceSynchronize();
         if (err == hipSuccess) err = reanchor_azimuths(e);   // (they may start from the old template's)
@@ -1791,6 +1816,11 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     e->cols = cols;
     e->hmap_host = split_terrain(terrain_ft, rows, cols);
     rederive(e);   // model constants, and the constant-specialised kernel when they are the baked ones
+    if (!gear_layout_ok(e->Pf)) {
+        delete e;
+        return fail(HG_E_INVALID, "landing gear: the step kernels need the nose wheel on the centre line and "
+                                  "the mains mirrored about it on one waterline");
+    }
     rc = build_template(e);
     if (rc != HG_OK) { delete e; return rc; }
     auto cleanup = [&](hipError_t err, const char* what) {
@@ -1823,8 +1853,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if ((err = hipMalloc(&e->pd_dev, sizeof(Params<double>))) != hipSuccess) return cleanup(err, "hipMalloc params64");
     if ((err = hipMemcpy(e->pd_dev, &e->Pd, sizeof(e->Pd), hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy params64");
-    if ((err = hipMalloc(&e->retrim_count, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim");
-    if ((err = hipMemset(e->retrim_count, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim");
+    if ((err = hipMalloc(&e->retrim_count, 5 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim");
+    if ((err = hipMemset(e->retrim_count, 0, 5 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim");
     if ((err = hipMalloc(&e->retrim_ring, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim ring");
     if ((err = hipMemset(e->retrim_ring, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim ring");
     if (cfg->reset_mode == HG_RESET_RETRIM) {
@@ -1985,6 +2015,7 @@ int32_t hg_reset(hg_env* e, const uint8_t* mask, float* obs, void* stream) {
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
         r.bad_jobs = e->retrim_count + 2;
+        r.solve_stats = e->retrim_count + 3;
         HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), s));
         HIP_TRY(hipGetLastError());
     }
@@ -2086,6 +2117,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
         r.bad_jobs = e->retrim_count + 2;
+        r.solve_stats = e->retrim_count + 3;
         r.ov = 1;
         r.tmpl = reinterpret_cast<const float*>(e->tmpl_dev);
         r.tmpl_env = e->Pf.env_templates ? e->tmpl_env : nullptr;
@@ -2108,6 +2140,7 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.n = e->n;
         r.fail_count = e->retrim_count + 1;
         r.bad_jobs = e->retrim_count + 2;
+        r.solve_stats = e->retrim_count + 3;
         HIP_TRY(hgk::launch_retrim(r, retrim_grid(e->n), s));
     }
     HIP_TRY(hipGetLastError());
@@ -2190,6 +2223,7 @@ int32_t hg_trim_batch(hg_env* e, const float* wind, int64_t count, float* state,
     r.out_action = action;
     r.out_obs = obs;
     r.out_status = status;
+    r.solve_stats = e->retrim_count + 3;
     HIP_TRY(hgk::launch_retrim(r, retrim_grid(count), (hipStream_t)stream));
     HIP_TRY(hipGetLastError());
     return HG_OK;
@@ -2210,7 +2244,12 @@ int32_t hg_trim_conds_batch(hg_env* e, const hg_trim_cond* conds, int64_t count,
         e->setup_batch_cap = count;
     }
     std::vector<hg::TrimSetup> host((size_t)count);
-    for (int64_t j = 0; j < count; ++j) host[j] = trim_setup(e->Pd, e->hmap_host.data(), conds[j]);
+    for (int64_t j = 0; j < count; ++j) {
+        host[j] = trim_setup(e->Pd, e->hmap_host.data(), conds[j]);
+        // the env condition's pivot order as the first choice (the residual test rejects it where
+        // another condition's Jacobian needs other pivots, and the solve searches)
+        memcpy(host[j].piv, e->setup.piv, sizeof(host[j].piv));
+    }
     hipStream_t s = (hipStream_t)stream;
     HIP_TRY(hipMemcpyAsync(e->setup_batch, host.data(), sizeof(hg::TrimSetup) * count, hipMemcpyHostToDevice, s));
     hgk::RetrimArgs r;
@@ -2224,6 +2263,7 @@ int32_t hg_trim_conds_batch(hg_env* e, const hg_trim_cond* conds, int64_t count,
     r.out_action = action;
     r.out_obs = obs;
     r.out_status = status;
+    r.solve_stats = e->retrim_count + 3;
     HIP_TRY(hgk::launch_retrim(r, retrim_grid(count), s));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(s));   // the host staging of the setups is released on return
@@ -2257,6 +2297,17 @@ int32_t hg_retrim_failures(hg_env* e, int64_t* count) {
     int32_t v = 0;
     HIP_TRY(hipMemcpy(&v, e->retrim_count + 1, sizeof(int32_t), hipMemcpyDeviceToHost));
     *count = v;
+    return HG_OK;
+}
+
+int32_t hg_debug_retrim_solves(hg_env* e, int64_t* counts) {
+    if (!e || !counts) return fail(HG_E_INVALID, "bad env or counts");
+    DevGuard dev_guard(e);
+    if (!dev_guard.ok) return fail(HG_E_HIP, "hipSetDevice to the handle's device failed");
+    int32_t v[2] = {0, 0};
+    HIP_TRY(hipMemcpy(v, e->retrim_count + 3, sizeof(v), hipMemcpyDeviceToHost));
+    counts[0] = v[0];
+    counts[1] = v[1];
     return HG_OK;
 }
 

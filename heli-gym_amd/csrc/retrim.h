@@ -79,6 +79,8 @@ struct RetrimArgs {
     const float* tmpl;      // ov: the shared reset template (heli 18 | carry 4 | obs 17) ...
     const float* tmpl_env;  // ... or the per-env ones [N][39] (Params::env_templates), else NULL
     int32_t* bad_jobs;      // env mode: job records naming no env (or a count past N), skipped and counted
+    int32_t* solve_stats;   // [0] Newton solves tried with the setup's pivot order, [1] of them rejected
+                            // by the residual test (and searched instead); may be NULL
 };
 
 // Launch retrim_kernel (one 64-lane block per trim, up to `grid` blocks looping over the jobs).

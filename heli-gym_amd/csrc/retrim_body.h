@@ -6,6 +6,7 @@
 #pragma once
 
 #include "retrim.h"
+#include "gj_mfma.h"
 
 namespace hgk {
 namespace {
@@ -162,6 +163,16 @@ __device__ __forceinline__ void gj_steps(double (&A)[16], double& b, uint32_t& l
 // with a quarter of the elementwise work and of the LDS reads per lane.
 #ifndef HG_GJ_SPLIT
 #define HG_GJ_SPLIT 2
+#endif
+// HG_GJ_MFMA (default): the blocked solve of gj_mfma.h (four panels, one v_mfma_f64_16x16x4_f64 each)
+// instead of the unblocked one below (HG_GJ_MFMA=0 for A/B).  HG_GJ_STATIC (default): first with the
+// pivot order of the host's trim of the same condition (gjs_solve, no pivot search), accepted when its
+// residual is that of a backward-stable solve, else searched (gjm_solve).
+#ifndef HG_GJ_MFMA
+#define HG_GJ_MFMA 1
+#endif
+#ifndef HG_GJ_STATIC
+#define HG_GJ_STATIC 1
 #endif
 template <int C>
 __device__ __forceinline__ void gjs_step(double (&A4)[4], double& b, uint32_t& live, int& mycol, int i, int l) {
@@ -374,6 +385,8 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     __shared__ double sXc[HG_RT_XLDS ? 16 : 1];   // HG_RT_XLDS: the current iterate
     __shared__ double sExt[7];       // observation terms of the current iterate
     __shared__ double sRow[HG_GJ_LDS ? 64 * kRowStride : 2];   // HG_GJ_LDS: the rows of the solve
+    __shared__ double sImg[HG_GJ_MFMA ? 16 * kImgStride : 2];  // HG_GJ_MFMA: the system's image per panel
+    __shared__ int8_t sPiv[64];      // HG_GJ_STATIC: the setup's pivot order per Newton step
     const int l = threadIdx.x;
     const hg::Params<double>& P = *a.P;
     const double eps = hg::kTrimEps;
@@ -429,6 +442,10 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
         }
         const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];
         if (l < 16) sYt[l] = T.yt[l];   // (read after the first round's lds_order)
+#if HG_GJ_MFMA && HG_GJ_STATIC
+        sPiv[l] = T.piv[l >> 4][l & 15];
+        const bool use_piv = T.piv[0][0] >= 0;
+#endif
         double W[3] = {P.wm[0], P.wm[1], P.wm[2]};   // NULL wind: the mean wind (helicopter.py:55)
         if (a.recs) {
             W[0] = (double)__int_as_float(rec.y);
@@ -538,7 +555,34 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             asm volatile("; ACC_END");
 #endif
             RSTAMP(3 + 4 * round, "v"(ye[0]));
-#if HG_GJ_SPLIT
+#if HG_GJ_MFMA
+            {
+                bool solved = false;
+#if HG_GJ_STATIC
+                if (use_piv) {
+                    solved = gjs_solve(sE, kEStride, 0.5 / eps, src, sYt, sPiv + 16 * (it < 3 ? it : 3), sImg, sX, l);
+                    if (l == 0 && a.solve_stats) {
+                        atomicAdd(a.solve_stats, 1);
+                        if (!solved) atomicAdd(a.solve_stats + 1, 1);
+                    }
+                    lds_order();   // (the searched solve rewrites the image and x the residual test read)
+                }
+#endif
+                if (!solved) gjm_solve(sE, kEStride, 0.5 / eps, src, sYt, sImg, sX, l);
+                lds_order();
+                bool fin = true;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+#if HG_RT_XLDS
+                    fin = fin && isfinite(sX[k]);
+#else
+                    dir[k] = sX[k];
+                    fin = fin && isfinite(dir[k]);
+#endif
+                }
+                if (!fin) { ok = false; break; }
+            }
+#elif HG_GJ_SPLIT
             {
                 const int i = l & 15, q = l >> 4;
                 double A4[4], Em4[4];

@@ -24,6 +24,10 @@ struct TrimSetup {
     // functions of the fixed entries alone, evaluated once per trim condition (trim_precompute):
     double rho_irho[2];  // density at the trim altitude and its reciprocal
     double s_psi, c_psi; // sin / cos of the fixed yaw
+    // the pivot order partial pivoting took in the host's trim of this condition at the mean wind,
+    // per Newton step (the 4th for every later one): piv[k][C] = the row that pivots column C.  The
+    // device trim's solve tries it first (gj_mfma.h gjs_solve; piv[0][0] < 0: no order, search).
+    int8_t piv[4][16];
 };
 
 // The per-condition constants of TrimSetup, from its base state (the same functions the model
@@ -89,8 +93,10 @@ HD double trim_residual(const double y[16], const double yt[16]) {
 
 // np.linalg.inv(dydx) @ r (:524-527) via Gauss-Jordan with partial pivoting.  Returns false for a
 // singular or non-finite pivot.
-HD bool solve16(double A[16][16], const double r[16], double v[16]) {
+HD bool solve16(double A[16][16], const double r[16], double v[16], int8_t* piv = nullptr) {
     double M[16][17];
+    int8_t idx[16];   // the original row now in row i (piv: the row that pivoted column i)
+    for (int i = 0; i < 16; ++i) idx[i] = (int8_t)i;
     for (int i = 0; i < 16; ++i) {
         for (int j = 0; j < 16; ++j) M[i][j] = A[i][j];
         M[i][16] = r[i];
@@ -100,12 +106,16 @@ HD bool solve16(double A[16][16], const double r[16], double v[16]) {
         for (int i = c + 1; i < 16; ++i)
             if (fabs(M[i][c]) > fabs(M[p][c])) p = i;
         if (M[p][c] == 0.0 || !isfinite(M[p][c])) return false;
-        if (p != c)
+        if (p != c) {
             for (int j = 0; j < 17; ++j) {
                 const double t = M[c][j];
                 M[c][j] = M[p][j];
                 M[p][j] = t;
             }
+            const int8_t t = idx[c];
+            idx[c] = idx[p];
+            idx[p] = t;
+        }
         const double rinv = 1.0 / M[c][c];   // one division per pivot step (the device's too)
         for (int j = c; j < 17; ++j) M[c][j] *= rinv;
         for (int i = 0; i < 16; ++i) {
@@ -116,6 +126,8 @@ HD bool solve16(double A[16][16], const double r[16], double v[16]) {
         }
     }
     for (int i = 0; i < 16; ++i) v[i] = M[i][16];
+    if (piv)
+        for (int i = 0; i < 16; ++i) piv[i] = idx[i];
     return true;
 }
 

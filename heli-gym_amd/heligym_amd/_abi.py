@@ -107,6 +107,7 @@ _SIGS = {
     "hg_retrim_failures": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "hg_set_retrim_overlap": (ctypes.c_int32, [_P, ctypes.c_int32]),
     "hg_debug_retrim_invalid": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
+    "hg_debug_retrim_solves": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "hg_debug_queues": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int32)]),
     "hg_debug_launches": (ctypes.c_int32, [_P, ctypes.POINTER(ctypes.c_int64)]),
     "hg_clock_stamp": (ctypes.c_int32, [_P, _P]),

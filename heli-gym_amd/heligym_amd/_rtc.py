@@ -25,7 +25,7 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
          "-fno-hip-fp32-correctly-rounded-divide-sqrt", "-fgpu-flush-denormals-to-zero", "-fno-slp-vectorize",
          "-ffp-contract=on", "-Wno-unused-result",
          "-mllvm", "-amdgpu-kernarg-preload-count=6", "-mllvm", "-disable-vector-combine",
-         "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
+         "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "-mllvm", "-amdgpu-mfma-vgpr-form"]
 PARAMS_BYTES_MAX = 4096
 
 
@@ -81,10 +81,12 @@ def build(lib, cfg, rows, cols, task):
                os.path.join(CSRC, "step_rtc.hip")]
         try:
             r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"step specialisation failed ({' '.join(cmd)}):\n{r.stderr[-2000:]}")
+            os.replace(tmp, path)   # atomic: concurrent builders of the same key agree
         finally:
             os.unlink(inc)
-        if r.returncode != 0:
-            raise RuntimeError(f"step specialisation failed ({' '.join(cmd)}):\n{r.stderr[-2000:]}")
-        os.replace(tmp, path)   # atomic: concurrent builders of the same key agree
+            if os.path.exists(tmp):   # a failed or interrupted build leaves no stray code object
+                os.unlink(tmp)
     # (hg_load_specialized also checks the image the code object was built with against img)
     return path, img

@@ -608,6 +608,13 @@ class HeliVecEnv(*_VEC_BASES):
         self._check(self.lib.hg_debug_launches(self._h, out))
         return dict(zip(self.LAUNCH_KINDS, (int(v) for v in out)))
 
+    def retrim_solve_stats(self):
+        """Diagnostic: (solves tried with the host trim's pivot order, of them re-solved with the pivot
+        search after failing the residual test) over the device trims of this env (hg_debug_retrim_solves)."""
+        c = (ctypes.c_int64 * 2)()
+        self._check(self.lib.hg_debug_retrim_solves(self._h, c))
+        return int(c[0]), int(c[1])
+
     def retrim_invalid_jobs(self):
         """Diagnostic: re-trim job records that named no env (skipped); 0 in a correct run."""
         c = ctypes.c_int64()
@@ -621,6 +628,11 @@ class HeliVecEnv(*_VEC_BASES):
         t = self.torch
         if out is None:
             out = t.empty((self.num_envs, 3), dtype=t.float32, device=self.device)
+        elif (tuple(out.shape) != (self.num_envs, 3) or out.dtype != t.float32 or out.device != t.device(self.device)
+              or not out.is_contiguous()):
+            # the kernel writes 3 * num_envs floats: never hand it a buffer that does not hold them
+            raise ValueError(f"debug_eta: out must be a contiguous float32 ({self.num_envs}, 3) tensor on "
+                             f"{self.device}, got {tuple(out.shape)} {out.dtype} on {out.device}")
         self._check(self.lib.hg_debug_eta(self._h, _ptr(out), self._stream()))
         return out
 

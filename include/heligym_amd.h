@@ -298,6 +298,12 @@ int32_t hg_retrim_failures(hg_env* env, int64_t* count);
  * instead of indexing the state with them; 0 in a correct run.  Synchronises with the device. */
 int32_t hg_debug_retrim_invalid(hg_env* env, int64_t* count);
 
+/* Diagnostic: the device trim's Newton solves since creation (every re-trim, hg_trim_batch and
+ * hg_trim_conds_batch of this env): counts[0] solved with the pivot order of the host's trim of the
+ * env's condition (gj_mfma.h gjs_solve), counts[1] of them rejected by the residual test and
+ * re-solved with the pivot search.  Synchronous (reads device counters). */
+int32_t hg_debug_retrim_solves(hg_env* env, int64_t* counts);
+
 /* Diagnostic: the re-trim job-count rings (out[0..2] the step re-trim ring, out[3..5] the overlapped
  * re-trim ring or -7, out[6..8] hg_reset's job count, failures, invalid jobs).  Synchronises. */
 int32_t hg_debug_queues(hg_env* env, int32_t* out);
@@ -344,7 +350,9 @@ int32_t hg_random_actions(hg_env* env, float* actions_dev, uint64_t seed, uint64
 int32_t hg_debug_eta(hg_env* env, float* eta_dev, void* stream);
 
 /* Diagnostic (known-answer tests): the device Philox4x32-10 on `count` rows of in_dev
- * {ctr0, ctr1, ctr2, ctr3, key0, key1} (u32) -> out_dev [count,4] u32. */
+ * {ctr0, ctr1, ctr2, ctr3, key0, key1} (u32) -> out_dev [count,4] u32.  It has no handle: it runs on
+ * the calling thread's current HIP device, and both buffers must be device memory of that device
+ * holding at least 6*count and 4*count words. */
 int32_t hg_debug_philox(const uint32_t* in_dev, uint32_t* out_dev, int64_t count, void* stream);
 
 /* Benchmark clock: one single-lane kernel on `stream` that writes the GPU's constant 100 MHz clock

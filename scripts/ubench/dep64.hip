@@ -32,6 +32,34 @@ __global__ void __launch_bounds__(64) k(double* out, unsigned long long* cyc, in
         if (K == 12) asm volatile(S16("v_add_u32 %0, %0, %1\n") : "+v"(u) : "v"(y));
         if (K == 13) asm volatile(S16("v_cmp_gt_u32 vcc, %1, %0\n v_cndmask_b32 %0, %0, %1, vcc\n") : "+v"(u) : "v"(y));
         if (K == 14) asm volatile(S16("v_cmp_gt_f64 vcc, %0, %1\n s_nop 0\n") : : "v"(a), "v"(m));
+        if (K == 15) {   // f64 MFMA 16x16x4, one dependent accumulator chain
+            typedef double d4 __attribute__((ext_vector_type(4)));
+            d4 acc = {a, b, c, d};
+            for (int r = 0; r < 16; ++r) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(m, n, acc, 0, 0, 0);
+            a = acc[0]; b = acc[1]; c = acc[2]; d = acc[3];
+        }
+        if (K == 16) {   // f64 MFMA 16x16x4, 4 independent accumulators
+            typedef double d4 __attribute__((ext_vector_type(4)));
+            d4 x0 = {a, b, c, d}, x1 = x0 + 1.0, x2 = x0 + 2.0, x3 = x0 + 3.0;
+            for (int r = 0; r < 4; ++r) {
+                x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(m, n, x0, 0, 0, 0);
+                x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(m, n, x1, 0, 0, 0);
+                x2 = __builtin_amdgcn_mfma_f64_16x16x4f64(m, n, x2, 0, 0, 0);
+                x3 = __builtin_amdgcn_mfma_f64_16x16x4f64(m, n, x3, 0, 0, 0);
+            }
+            a = x0[0] + x1[1]; b = x2[2] + x3[3];
+        }
+        if (K == 17)   // v_fma_f64 -> 2 v_readlane -> next v_fma_f64 reads the SGPR pair (a loop-carried chain)
+            asm volatile(S16("v_fma_f64 v[40:41], s[20:21], %0, %1\n v_readlane_b32 s20, v40, 5\n v_readlane_b32 s21, v41, 5\n")
+                         : : "v"(m), "v"(n) : "s20", "s21", "v40", "v41");
+        if (K == 18)   // v_cmp -> s_ff1 -> v_readlane with that lane -> v_mov (the pivot search's tail), chained
+            asm volatile(S16("v_cmp_eq_u32 s[22:23], %0, %1\n s_ff1_i32_b64 s24, s[22:23]\n v_readlane_b32 s25, %0, s24\n v_add_u32 %0, s25, %0\n")
+                         : "+v"(u) : "v"(y) : "s22", "s23", "s24", "s25");
+        if (K == 19) asm volatile(S16("v_mul_f64 %0, %0, %1\n") : "+v"(a) : "v"(m));
+        if (K == 20) {   // permlane16 swap chain
+            for (int r = 0; r < 16; ++r) { auto t = __builtin_amdgcn_permlane16_swap(u, v, false, false); u = t[0] + 1; v = t[1]; }
+        }
+        if (K == 21) asm volatile(S16("ds_bpermute_b32 %0, %1, %0\n s_waitcnt lgkmcnt(0)\n") : "+v"(u) : "v"(w));
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
     out[blockIdx.x * 64 + threadIdx.x] = a + b + c + d + u + v + w + x;
@@ -70,5 +98,12 @@ int main() {
     run<12>("v_add_u32, 1 dependent chain", 1);
     run<13>("v_cmp -> v_cndmask on vcc (per instr)", 2);
     run<14>("v_cmp_gt_f64 + s_nop 0 (per pair)", 1);
+    run<15>("v_mfma_f64_16x16x4, 1 dependent chain", 1);
+    run<16>("v_mfma_f64_16x16x4, 4 chains", 1);
+    run<17>("fma_f64 -> 2 readlane -> fma (per group)", 1);
+    run<18>("cmp -> s_ff1 -> readlane(lane s) -> add (per group)", 1);
+    run<19>("v_mul_f64, 1 dependent chain", 1);
+    run<20>("permlane16_swap chain (+add) (per swap)", 1);
+    run<21>("ds_bpermute + wait (per round trip)", 1);
     return 0;
 }

@@ -29,10 +29,10 @@ def torch():
     return t
 
 
-def _env(torch, n, **kw):
+def _env(torch, n, task="hover", **kw):
     from heligym_amd import HeliVecEnv
     kw.setdefault("seed", 0x5EED_7E4B_0000_0017)
-    return HeliVecEnv(n, task="hover", dt=0.01, autoreset=True, device="cuda:0", **kw)
+    return HeliVecEnv(n, task=task, dt=0.01, autoreset=True, device="cuda:0", **kw)
 
 
 def test_device_philox_matches_kat_and_host(torch):
@@ -91,6 +91,19 @@ def test_in_kernel_eta_matches_host_restatement(torch):
     tol = ETA_ABS + ETA_REL * np.abs(ref)
     print(f"\n[eta] max|d| {err.max():.3e}, max |d|/tol {(err / tol).max():.3f}")
     assert np.all(err <= tol), np.argwhere(err > tol)[:10]
+    env.close()
+
+
+def test_debug_eta_rejects_a_wrong_buffer(torch):
+    """debug_eta writes 3 * N floats: a buffer of another shape, dtype, device or layout is refused
+    before the kernel runs (ValueError), never written out of bounds."""
+    env = _env(torch, 100)
+    bad = [torch.zeros((99, 3), device="cuda:0"), torch.zeros((100, 3), dtype=torch.float64, device="cuda:0"),
+           torch.zeros((100, 3)), torch.zeros((3, 100), device="cuda:0").t()]
+    for out in bad:
+        with pytest.raises(ValueError):
+            env.debug_eta(out)
+    assert env.debug_eta().shape == (100, 3)
     env.close()
 
 
@@ -166,17 +179,19 @@ def _launch_kind(n, cus):
     return "lone-wave" if n <= 2 * 64 * 4 * cus else "bulk"
 
 
-@pytest.mark.parametrize("n", [4096, 65536, 262144])
-def test_in_kernel_noise_step_bitwise_equals_injected(torch, n):
+@pytest.mark.parametrize("n,task", [(4096, "hover"), (65536, "hover"), (262144, "hover"),
+                                    (262144, "forward_flight")])
+def test_in_kernel_noise_step_bitwise_equals_injected(torch, n, task):
     """The population stepped by the kernel the benchmark times at this size (in-kernel noise:
-    helper kernel at 4 096 envs, lone-wave at 65 536, bulk at 262 144) and a twin stepped by the
-    injected-noise kernel (the instantiation every oracle / golden parity test runs) fed the
+    helper kernel at 4 096 envs, lone-wave at 65 536, bulk at 262 144; BASELINE config 4 is the
+    262 144-env HeliForwardFlight population, helicopter_with_tasks.py:78-115) and a twin stepped by
+    the injected-noise kernel (the instantiation every oracle / golden parity test runs) fed the
     exported eta of the same step: observations, rewards, flags and info bits bitwise equal at every
     one of 400 steps (crashes, auto-resets, new episode keys), and the final state."""
     cus = torch.cuda.get_device_properties(0).multi_processor_count
     kind = _launch_kind(n, cus)
-    print(f"\n[{n} envs] in-kernel launch: {kind}")
-    a, b = _env(torch, n), _env(torch, n)
+    print(f"\n[{n} {task} envs] in-kernel launch: {kind}")
+    a, b = _env(torch, n, task), _env(torch, n, task)
     a.reset()
     b.reset()
     act = torch.empty((n, 4), dtype=torch.float32, device=a.device)
