@@ -1011,6 +1011,9 @@ def main():
                 s_rt, _, _, rs_rt = timer.run_counted(envr, repr_, 3)
                 del _kr
                 ov = amode == "next_step" and envr.set_retrim_overlap(True)
+                solves, searched = envr.retrim_solve_stats()
+                _, ctr_r = envr.get_state()
+                trims = int(ctr_r[:, 2].long().sum())
                 # a window without a reset would time the plain step, not the re-trim: no value then
                 secondary[name] = {
                     "envs": N, "value": N * Kr / s_rt if rs_rt > 0 else None, "unit": "env-steps/s",
@@ -1018,6 +1021,11 @@ def main():
                     "resets_in_window": rs_rt, "aged_steps": aged_r, "autoreset_mode": amode,
                     "steps": Kr, "retrim_failures": envr.retrim_failures(),
                     "retrim_invalid_jobs": envr.retrim_invalid_jobs(),
+                    "trim_solves": {"trims": trims, "newton_solves": solves, "searched": searched,
+                                    "solves_per_trim": solves / trims if trims else None,
+                                    "note": "over the env's life (ageing + windows): Newton solves tried with the "
+                                            "host trim's pivot order, and those the residual test sent to the "
+                                            "pivot search (csrc/gj_mfma.h)"},
                     "note": "reset_mode='retrim': each auto-reset re-trimmed on the device (Newton trim against the "
                             "env's last wind, the reference's reset from episode 2 on), hipGraph"
                             + ("; next-step auto-reset (make_vec's configuration): the episodes a step ends are "

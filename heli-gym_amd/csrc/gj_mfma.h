@@ -192,27 +192,50 @@ __device__ __forceinline__ void gjm_solve(const double* sE, int es, double s, in
 // ---------------------------------------------------------------------------------------------------
 // The same blocked solve with the pivot order given (round 6): the rows are loaded permuted so that
 // pivot step C pivots lane C (row perm[C] of the system) on column C, the order partial pivoting took
-// on the host's trim of the same condition (hg::TrimSetup::piv, the Newton step's own order).  With
-// the pivot lane known at compile time there is no search: the pivot row reaches the other rows with
-// a DPP row_newbcast (v_mov_b64_dpp / v_fmac_f64_dpp: one instruction per element instead of two
-// readlanes and an fma), and a step is the pivot's reciprocal, the multipliers and three fused
-// updates.  Rows are scaled as they pivot (g = 1/pivot - 1 at the pivot row; the system carries
-// J - I on its diagonal so that the same fused update serves every row), so the right-hand side ends
-// as x itself, x[C] in row C.  The three later panels' columns come out of a second MFMA already
-// replicated over the quarters (C rows of its A operand repeat each pivot row's column), and every
-// LDS address the panel needs is known before its pivots are: no lane shuffle and no LDS wait on the
-// step chain.
+// on the host's trim of the same condition (hg::TrimSetup::piv, that Newton step's own order).  With
+// the pivot lane known at compile time there is no search, and the pivot row reaches the other rows
+// with a DPP row_newbcast inside the instruction that uses it (v_rcp_f64_dpp, v_fmac_f64_dpp): a step
+// is the pivot's reciprocal (one Newton step), the multipliers, and one fused update per element.
+// Its dependent chain is five instructions.
+//   * Rows stay unscaled (the pivot row's multiplier is 0); x[C] = b[C] / pivot at the end.
+//   * The augmented columns are one register: quarter q carries column q of Aug = E[:, P] (the
+//     lazily injected identity column e_{4p+q} from the panel's start), and one v_fmac_f64_dpp per
+//     step updates all four quarters -- the broadcast from lane C of each quarter is exactly the pivot
+//     row's entry of that quarter's column.  The MFMAs then take C with the panel's pivot rows zeroed:
+//     (J - S S^T J) + Aug S^T J = E J.
+//   * The next panel's columns come out of a second MFMA already replicated over the quarters (the
+//     rows of its A operand repeat each pivot row's entry of those columns), and every LDS address a
+//     panel needs is known before its pivots are: no lane shuffle and no LDS wait on the step chain.
 //
 // A given pivot order is not partial pivoting for this Jacobian, so the solution is accepted only if
 // its residual is that of a backward-stable solve: |J x - b|_i <= kGjsTol (sum_c |J_ic| |x_c| + |b_i|)
-// for every row (the searched solve's residuals are below 1e-16 of that scale, profiles/
-// r06_gj_solve.txt); otherwise the caller runs the searched solve (gjm_solve).
+// for every row (the pivoted solves' residuals are orders of magnitude below that scale,
+// profiles/r06_gj_solve.txt); otherwise the caller runs the searched solve (gjm_solve).
 constexpr double kGjsTol = 1e-13;
+#ifndef GJS_RCP_DPP
+#define GJS_RCP_DPP 0
+#endif
 
+// Hazards: the compiler pads only around the instructions it generates.  Each asm below starts with
+// the 2 wait states a DPP read needs after a VALU write of its source; the other hazards around them
+// are kept out by construction -- no asm reads an MFMA result (a panel's first broadcast of the
+// MFMA's columns is the builtin form, which the compiler pads, and the chain after it outlasts the
+// MFMA's latency before any asm reads the other columns), and the MFMA's B operand gets its last
+// update from the builtin form too.
 template <int C>
 __device__ __forceinline__ double gjs_bcast(double v) {   // v of lane C of each 16-lane row
     double r;
     asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "n"(C & 15));
+    return r;
+}
+template <int C>
+__device__ __forceinline__ double gjs_bcast_c(double v) {   // the same, compiler-generated (hazards padded)
+    return __builtin_amdgcn_update_dpp(v, v, 0x150 + (C & 15), 0xF, 0xF, true);
+}
+template <int C>
+__device__ __forceinline__ double gjs_rcp_bcast(double v) {   // v_rcp_f64 of lane C's v
+    double r;
+    asm("s_nop 1\n\tv_rcp_f64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "n"(C & 15));
     return r;
 }
 template <int C>
@@ -232,19 +255,26 @@ __device__ __forceinline__ double gjs_quarter_sum(double x) {   // sum over the 
 }
 
 template <int PN, int K>
-__device__ __forceinline__ void gjs_step(double (&ct)[4], double (&a)[4]) {
+__device__ __forceinline__ void gjs_step(double (&c)[4], double& bop, double& myinv, int i) {
     constexpr int C = 4 * PN + K;
-    const double rinv = gjm_rcp(gjs_bcast<C>(ct[K]) + 1.0);   // 1 / J[C][C] (ct holds J - I on the diagonal)
-    const double g = -ct[K] * rinv;                           // -J[i][C] / pivot; 1 / pivot - 1 at row C
+    const double p = K == 0 ? gjs_bcast_c<C>(c[K]) : gjs_bcast<C>(c[K]);   // the pivot J[C][C]
+#if GJS_RCP_DPP
+    double r = gjs_rcp_bcast<C>(c[K]);
+#else
+    double r = __builtin_amdgcn_rcp(p);
+#endif
+    r = fma(r, fma(-p, r, 1.0), r);                  // one Newton step: within 1e-14 (the residual test guards)
+    const double cz = i == C ? 0.0 : c[K];           // (off the chain) the pivot row is not updated
+    const double g = -cz * r;                        // -J[i][C] / pivot
 #pragma unroll
-    for (int j = K + 1; j < 4; ++j) gjs_fmac_bcast<C>(ct[j], g);
-#pragma unroll
-    for (int j = 0; j < K; ++j) gjs_fmac_bcast<C>(a[j], g);
-    a[K] = g;
-    GJM_STAMP(8 * PN + 2 + K, ct[K < 3 ? K + 1 : 3]);
+    for (int j = K + 1; j < 4; ++j) gjs_fmac_bcast<C>(c[j], g);
+    if constexpr (K < 3) gjs_fmac_bcast<C>(bop, g);  // quarter q: column q of Aug
+    else bop = fma(gjs_bcast_c<C>(bop), g, bop);     // (the MFMA's B operand: a padded write)
+    myinv = i == C ? r : myinv;
+    GJM_STAMP(8 * PN + 2 + K, c[K < 3 ? K + 1 : 3]);
 }
 
-// the LDS image of the system (J - I) for panel PN's MFMA operands, written at its start
+// the LDS image of the system for panel PN's MFMA operands, written at its start
 __device__ __forceinline__ void gjs_image(const gjm_d4& R, double* sImg, int i, int q) {
     double* row = sImg + i * kImgStride + q;
     row[0] = R[0];
@@ -268,31 +298,30 @@ struct GjsOps {   // panel PN's MFMA operands, read from its image as soon as it
 };
 
 template <int PN>
-__device__ __forceinline__ void gjs_panel(gjm_d4& R, double (&ct)[4], GjsOps<PN>& ops, double* sImg, int i, int q) {
-    GJM_STAMP(8 * PN, ct[0]);
-    double a[4];
-    gjs_step<PN, 0>(ct, a);
-    gjs_step<PN, 1>(ct, a);
+__device__ __forceinline__ void gjs_panel(gjm_d4& R, double (&c)[4], GjsOps<PN>& ops, double& myinv, double* sImg,
+                                          int i, int q) {
+    GJM_STAMP(8 * PN, c[0]);
+    double bop = i == 4 * PN + q ? 1.0 : 0.0;   // Aug's columns before the panel: the identity's
+    gjs_step<PN, 0>(c, bop, myinv, i);
+    gjs_step<PN, 1>(c, bop, myinv, i);
     if constexpr (PN > 0) {   // this panel's image (the previous MFMA's system), off the step chain
         gjs_image(R, sImg, i, q);
         ops.read(sImg, i, q);
     }
-    gjs_step<PN, 2>(ct, a);
-    gjs_step<PN, 3>(ct, a);
-    double bop = a[0];   // B[k = q][col i] = a_q[i]
-    bop = q == 1 ? a[1] : bop;
-    bop = q == 2 ? a[2] : bop;
-    bop = q == 3 ? a[3] : bop;
+    gjs_step<PN, 2>(c, bop, myinv, i);
+    gjs_step<PN, 3>(c, bop, myinv, i);
     GJM_STAMP(8 * PN + 6, bop);
+    const bool prow = (i >> 2) == PN;   // the panel's pivot rows: zero in C (E J = (J - S S^T J) + Aug S^T J)
     if constexpr (PN < 3) {   // the next panel's columns first: the step chain waits for them only
-        const gjm_d4 c2 = {ops.c2[0], ops.c2[1], ops.c2[2], ops.c2[3]};
+        const gjm_d4 c2 = {prow ? 0.0 : ops.c2[0], prow ? 0.0 : ops.c2[1], prow ? 0.0 : ops.c2[2], prow ? 0.0 : ops.c2[3]};
         const gjm_d4 nx = __builtin_amdgcn_mfma_f64_16x16x4f64(ops.a2op, bop, c2, 0, 0, 0);
-        ct[0] = nx[0];
-        ct[1] = nx[1];
-        ct[2] = nx[2];
-        ct[3] = nx[3];
+        c[0] = nx[0];
+        c[1] = nx[1];
+        c[2] = nx[2];
+        c[3] = nx[3];
     }
-    R = __builtin_amdgcn_mfma_f64_16x16x4f64(ops.aop, bop, R, 0, 0, 0);
+    const gjm_d4 rz = {prow ? 0.0 : R[0], prow ? 0.0 : R[1], prow ? 0.0 : R[2], prow ? 0.0 : R[3]};
+    R = __builtin_amdgcn_mfma_f64_16x16x4f64(ops.aop, bop, rz, 0, 0, 0);
 }
 
 // Solve with the pivot order perm (perm[C] = the row that pivots column C).  Returns whether the
@@ -301,11 +330,11 @@ __device__ __forceinline__ bool gjs_solve(const double* sE, int es, double s, in
                                           const int8_t* perm, double* sImg, double* sX, int l) {
     const int i = l & 15, q = l >> 4;
     const int pi = perm[i];
-    double ct[4], m[4], e[3], me[3];
+    double c[4], m[4], e[3], me[3];
     gjm_d4 R;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        ct[k] = sE[k * es + pi];
+        c[k] = sE[k * es + pi];
         m[k] = sE[(k + 16) * es + pi];
     }
 #pragma unroll
@@ -315,39 +344,46 @@ __device__ __forceinline__ bool gjs_solve(const double* sE, int es, double s, in
     }
     const double b = sE[src * es + pi] - sYt[pi];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) ct[k] = (ct[k] - m[k]) * s - (i == k ? 1.0 : 0.0);
+    for (int k = 0; k < 4; ++k) c[k] = (c[k] - m[k]) * s;
     R[0] = b;
 #pragma unroll
-    for (int v = 1; v < 4; ++v) R[v] = (e[v - 1] - me[v - 1]) * s - (i == q + 4 * v ? 1.0 : 0.0);
+    for (int v = 1; v < 4; ++v) R[v] = (e[v - 1] - me[v - 1]) * s;
+    const double j0[4] = {c[0], c[1], c[2], c[3]};   // the system as given, for the residual test
+    const double j1[3] = {R[1], R[2], R[3]};
     gjs_image(R, sImg, i, q);
     GjsOps<0> o0;
     o0.read(sImg, i, q);
     GjsOps<1> o1;
     GjsOps<2> o2;
     GjsOps<3> o3;
-    gjs_panel<0>(R, ct, o0, sImg, i, q);
-    gjs_panel<1>(R, ct, o1, sImg, i, q);
-    gjs_panel<2>(R, ct, o2, sImg, i, q);
-    gjs_panel<3>(R, ct, o3, sImg, i, q);
+    double myinv = 0.0;
+    gjs_panel<0>(R, c, o0, myinv, sImg, i, q);
+    gjs_panel<1>(R, c, o1, myinv, sImg, i, q);
+    gjs_panel<2>(R, c, o2, myinv, sImg, i, q);
+    gjs_panel<3>(R, c, o3, myinv, sImg, i, q);
     GJM_STAMP(32, R[0]);
-    if (l < 16) sX[i] = R[0];
-    // the residual of the permuted system: J (recomputed from the evaluations, the same operations)
-    // times x, against b
+    if (l < 16) sX[i] = R[0] * myinv;
+    // the residual of the permuted system: J x - b from the system as given
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    double dot = 0.0, mag = 0.0;
+    double x0[4], xs[3];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        const int c = q + 4 * v;
-        const double J = (sE[c * es + pi] - sE[(c + 16) * es + pi]) * s;
-        const double x = sX[c];
-        dot = fma(J, x, dot);
-        mag = fma(fabs(J), fabs(x), mag);
+    for (int k = 0; k < 4; ++k) x0[k] = sX[k];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) xs[v - 1] = sX[q + 4 * v];
+    double dot = 0.0, mag = 0.0, dot0 = 0.0, mag0 = 0.0;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+        dot = fma(j1[v], xs[v], dot);
+        mag = fma(fabs(j1[v]), fabs(xs[v]), mag);
     }
-    dot = gjs_quarter_sum(dot);
-    mag = gjs_quarter_sum(mag);
-    const double r = dot - b;
-    const bool good = fabs(r) <= kGjsTol * (mag + fabs(b));   // (false for a non-finite x)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // columns 0..3: every quarter holds the whole row part
+        dot0 = fma(j0[k], x0[k], dot0);
+        mag0 = fma(fabs(j0[k]), fabs(x0[k]), mag0);
+    }
+    const double r = (gjs_quarter_sum(dot) + dot0) - b;
+    const bool good = fabs(r) <= kGjsTol * ((gjs_quarter_sum(mag) + mag0) + fabs(b));   // (false for a non-finite x)
     GJM_STAMP(33, r);
     return __ballot(!good) == 0;
 }

@@ -868,14 +868,19 @@ __global__ __launch_bounds__(128 * HG_HELPER, 1) void step_help_kernel(float* __
 // two waves per SIMD (<= 256 VGPRs), so at one step wave per SIMD a trim wave shares a SIMD with a
 // step wave; the trims, dispatched first, are the long pole.  One queue and no cross-stream events:
 // dependent work on another queue waited about 10 us per hop on MI355X (scripts/r04_ov_trace.py).
+// The leading (preloaded) arguments are the trims' job count, records, setup and model constants
+// (r.count, r.recs, r.T, r.P): the trim waves are the long pole and request them at once; the step
+// waves read the rest of their arguments from the argument segment instead.
 template <int TASK, bool BAKED>
 __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2))) void step_ov_kernel(
-    float* __restrict__ state_p, int64_t n_p, uint64_t seed_p, int64_t envoff_p, ParamArg Pa,
-    const Template<float>* __restrict__ Tp, const StepArgs a, const hgk::RetrimArgs r, int32_t tb) {
+    const int32_t* __restrict__ rcount, const int4* __restrict__ rrecs, const hg::TrimSetup* __restrict__ rT,
+    const hg::Params<double>* __restrict__ rP, float* __restrict__ state_p, int64_t n_p, uint64_t seed_p,
+    int64_t envoff_p, ParamArg Pa, const Template<float>* __restrict__ Tp, const StepArgs a, const hgk::RetrimArgs r,
+    int32_t tb) {
     if ((int32_t)blockIdx.x < tb) {
         // retrim_jobs treats threadIdx.x as the lane of one wave (Jacobian column, trial, LDS rows):
         // a trim block is its first wave (the others, with HG_STEP_BLOCK > 64, leave at once)
-        if (kStepBlock == 64 || threadIdx.x < 64) hgk::retrim_jobs(r, blockIdx.x, tb);
+        if (kStepBlock == 64 || threadIdx.x < 64) hgk::retrim_jobs(r, blockIdx.x, tb, rcount, rrecs, rT, rP, 0);
         return;
     }
     step_body<TASK, false, true, true, false, BAKED, false>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a,
@@ -1648,7 +1653,7 @@ static void launch_step_ov(const hg_env* e, hipStream_t s, const StepArgs& a, co
     const int32_t tb = ov_trim_blocks(e->n);
     const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock) + (unsigned)tb;
     auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(kStepBlock), 0, s, STEP_KARGS(e), a, r, tb);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kStepBlock), 0, s, r.count, r.recs, r.T, r.P, STEP_KARGS(e), a, r, tb);
     };
     switch (e->cfg.task) {
         case HG_TASK_HOVER: e->baked ? go(step_ov_kernel<HG_TASK_HOVER, true>) : go(step_ov_kernel<HG_TASK_HOVER, false>); break;

@@ -26,8 +26,13 @@ namespace {
 #ifndef HG_RETRIM_WAVES
 #define HG_RETRIM_WAVES 2
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WAVES))) void retrim_kernel(const RetrimArgs a) {
-    retrim_jobs(a, blockIdx.x, gridDim.x);
+// count_p / recs_p / T_p / P_p / Tstride_p = a.count / a.recs / a.T / a.P / a.setup_stride: leading
+// arguments, preloaded into SGPRs (__graft_entry__.py builds this translation unit with
+// -amdgpu-kernarg-preload-count=5)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HG_RETRIM_WAVES))) void retrim_kernel(
+    const int32_t* count_p, const int4* recs_p, const hg::TrimSetup* T_p, const hg::Params<double>* P_p,
+    int32_t Tstride_p, const RetrimArgs a) {
+    retrim_jobs(a, blockIdx.x, gridDim.x, count_p, recs_p, T_p, P_p, Tstride_p);
 }
 
 
@@ -54,7 +59,7 @@ extern "C" int hg_debug_rt_log_serial(void* dst, int64_t bytes, int32_t clear) {
 #endif
 
 hipError_t launch_retrim(const RetrimArgs& a, unsigned grid, hipStream_t stream) {
-    hipLaunchKernelGGL(retrim_kernel, dim3(grid), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(retrim_kernel, dim3(grid), dim3(64), 0, stream, a.count, a.recs, a.T, a.P, a.setup_stride, a);
     return hipGetLastError();
 }
 

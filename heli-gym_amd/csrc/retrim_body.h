@@ -376,7 +376,17 @@ __device__ unsigned g_rt_dbg_n;
 #endif
 // The jobs first, first + stride, ... of a batch, one wave (this block) per trim: retrim_kernel and the
 // trim blocks of the overlapped next-step re-trim (heligym_amd.hip step_ov_kernel).
-__device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, int64_t stride) {
+// count_p / recs_p / T_p / P_p: a.count / a.recs / a.T / a.P, passed again as leading kernel
+// arguments, which the kernels have preloaded into SGPRs at wave launch (-amdgpu-kernarg-preload-count),
+// and Tstride_p = a.setup_stride: the job count, the first record, the first job's setup and a
+// prefetch of the model constants are all requested at once, before the kernel-argument segment has
+// arrived (round 6: each was a dependent memory round trip of the trim's start-up).
+__device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, int64_t stride, const int32_t* count_p,
+                                            const int4* recs_p, const hg::TrimSetup* T_p, const hg::Params<double>* P_p,
+                                            int32_t Tstride_p) {
+    // the trim is the launch's long pole: its wave issues first wherever it shares a SIMD (the
+    // overlapped launch's step waves, one per SIMD, have time to spare)
+    __builtin_amdgcn_s_setprio(3);
     // the +-eps evaluations E[j][k] of the current Newton step, row j (the evaluating lane) at a stride
     // of kEStride doubles: lane j's 16 writes of a 16-double stride all hit the same two banks
     __shared__ double sE[42 * kEStride];   // rows 32..41: the line-search trials' evaluations
@@ -405,10 +415,24 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     // read reads the model constants instead (any readable address) and discards them.
     int zero_v;
     asm volatile("v_mov_b32 %0, 0" : "=v"(zero_v));
+    // (a launch has at most one block per env, so recs_p[first] is a record; with no queue, no load)
+    int4 rec0_v = make_int4(-1, 0, 0, 0);
+    int32_t count_v = 0;
+    if (recs_p || count_p) {
+        const int32_t* any = count_p ? count_p : reinterpret_cast<const int32_t*>(recs_p);
+        rec0_v = (recs_p ? recs_p + first : reinterpret_cast<const int4*>(any))[zero_v];
+        count_v = any[zero_v];
+    }
     const bool has_rec0 = a.recs && first < a.n;
-    const int4 rec0_v = (has_rec0 ? a.recs + first : reinterpret_cast<const int4*>(a.P))[zero_v];
-    const int32_t count_v = (a.count ? a.count : reinterpret_cast<const int32_t*>(a.P))[zero_v];
 #endif
+    // the first job's setup (initial guess, targets, pivot order), and one lane per 64-byte line of the
+    // model constants (into the L2 for the first round's scalar loads; the value is only kept alive)
+    const hg::TrimSetup* T0 = T_p + (Tstride_p ? first : 0);
+    const double x0_l = T0->x0[l & 15];
+    const double yt_l = T0->yt[l & 15];
+    const int8_t piv_l = T0->piv[l >> 4][l & 15];
+    constexpr int kPWords = (int)(sizeof(hg::Params<double>) / 4);
+    const uint32_t pf = reinterpret_cast<const uint32_t*>(P_p)[min(16 * l, kPWords - 1)];
 #if HG_RT_VLOAD
     const int4 rec0 = has_rec0 ? make_int4(__builtin_amdgcn_readfirstlane(rec0_v.x), __builtin_amdgcn_readfirstlane(rec0_v.y),
                                            __builtin_amdgcn_readfirstlane(rec0_v.z), __builtin_amdgcn_readfirstlane(rec0_v.w))
@@ -441,11 +465,13 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             continue;
         }
         const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];
-        if (l < 16) sYt[l] = T.yt[l];   // (read after the first round's lds_order)
+        const bool j0 = job == first;   // (its setup requested at entry)
 #if HG_GJ_MFMA && HG_GJ_STATIC
-        sPiv[l] = T.piv[l >> 4][l & 15];
-        const bool use_piv = T.piv[0][0] >= 0;
+        const int8_t piv_v = j0 ? piv_l : T.piv[l >> 4][l & 15];
+        sPiv[l] = piv_v;
+        const bool use_piv = __builtin_amdgcn_readfirstlane(piv_v) >= 0;   // (lane 0: piv[0][0])
 #endif
+        if (l < 16) sYt[l] = j0 ? yt_l : T.yt[l];   // (read after the first round's lds_order)
         double W[3] = {P.wm[0], P.wm[1], P.wm[2]};   // NULL wind: the mean wind (helicopter.py:55)
         if (a.recs) {
             W[0] = (double)__int_as_float(rec.y);
@@ -466,12 +492,12 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
 #pragma unroll
         for (int k = 0; k < 16; ++k) ye[k] = 0.0;
 #if HG_RT_XLDS
-        if (l < 16) { sXc[l] = T.x0[l]; sX[l] = 0.0; }
+        if (l < 16) { sXc[l] = j0 ? x0_l : T.x0[l]; sX[l] = 0.0; }
         lds_order();
 #else
         double x[16], dir[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) { x[k] = T.x0[k]; dir[k] = 0.0; }
+        for (int k = 0; k < 16; ++k) { x[k] = j0 ? read_lane(x0_l, k) : T.x0[k]; dir[k] = 0.0; }
 #endif
         double tol = 0;
         int it = 0, kind = kRoundFirst, src = 32, round = 0;
@@ -678,6 +704,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
         RSTAMP(61, "v"(l));   // the write-out issued
         lds_order();   // the next job's writes come after this job's reads
     }
+    if (pf == 0x7FC00001u && jobs == -12345 && a.bad_jobs) atomicAdd(a.bad_jobs, 0);   // (keeps the prefetch)
 }
 
 }  // namespace

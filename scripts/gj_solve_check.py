@@ -152,6 +152,14 @@ def main():
             err = np.abs(x - ref).max(1) / (cond * eps * (np.abs(ref).max(1) + 1))
             print(f"[{name}] trim jacobians {label:13s} cycles median {np.median(cyc):.0f}  err/(cond eps |x|) max "
                   f"{err.max():.3g}  fell back {int(fb.sum())}")
+    lib.gj_dpp_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    vin = np.ascontiguousarray(np.arange(64, dtype=np.float64) + 1.5)
+    dout = np.zeros((64, 3))
+    assert lib.gj_dpp_check(vin.ctypes.data, dout.ctypes.data) == 0
+    src = vin.reshape(4, 16)[:, 3].repeat(16)
+    print("DPP row_newbcast:3 -- v_mov_b64 ok:", np.array_equal(dout[:, 0], src),
+          " v_rcp_f64 ok:", np.allclose(dout[:, 1], 1 / src, rtol=1e-7), "(own-lane rcp:", np.allclose(dout[:, 1], 1 / vin, rtol=1e-7), ")",
+          " v_fmac_f64 ok:", np.array_equal(dout[:, 2], vin + 2 * src))
     lib.gj_rcp_check.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     xs = np.ascontiguousarray(np.concatenate([rng.uniform(-50, 50, 100000), 10.0 ** rng.uniform(-6, 6, 100000)]))
     er = np.zeros((len(xs), 3))

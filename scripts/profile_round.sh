@@ -1,5 +1,6 @@
 # Profiles for the judged bench line: rocprofv3 kernel-trace --stats of the bench command, then
-# separate --pmc passes (traffic + issue counters).  Results -> gpurun_out/prof_<tag>/ and a
+# separate --pmc passes (traffic + issue counters).  BENCH_ARGS adds bench.py options (e.g.
+# "--reset-mode retrim --autoreset-mode next_step") and KERNEL_RE picks the kernel to summarise.  Results -> gpurun_out/prof_<tag>/ and a
 # summary profiles/<tag>_pmc_summary.json written by scripts/summarize_prof.py.
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -13,7 +14,7 @@ export TMPDIR=/tmp
 # is collected separately, age ${PMC_AGE:-20} s (the population is mixed after about 10 s, the
 # time-limit cohort aside)
 echo "[$TAG] trace"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o bench -- python3 bench.py --envs $N --dt $DT --task ${TASK:-hover} --steps ${TRACE_STEPS:-1000} --repeats 2 --no-secondary --no-cpu-baseline --no-parity > $D/trace.log 2>&1 || { echo "trace failed"; tail -20 $D/trace.log; exit 3; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o bench -- python3 bench.py --envs $N --dt $DT --task ${TASK:-hover} ${BENCH_ARGS:-} --steps ${TRACE_STEPS:-1000} --repeats 2 --no-secondary --no-cpu-baseline --no-parity > $D/trace.log 2>&1 || { echo "trace failed"; tail -20 $D/trace.log; exit 3; }
 i=0
 for set in "FETCH_SIZE" "WRITE_SIZE" \
            "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS" \
@@ -21,7 +22,7 @@ for set in "FETCH_SIZE" "WRITE_SIZE" \
            "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   echo "[$TAG] pmc pass $i: $set"
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set --output-format csv -d $D/pmc$i -o run -- python3 bench.py --envs $N --dt $DT --task ${TASK:-hover} --steps 200 --warmup 20 --repeats 1 --age-seconds ${PMC_AGE:-20} --no-secondary --no-cpu-baseline --no-parity > $D/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $D/pmc$i.log; exit 4; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $set --output-format csv -d $D/pmc$i -o run -- python3 bench.py --envs $N --dt $DT --task ${TASK:-hover} ${BENCH_ARGS:-} --steps 200 --warmup 20 --repeats 1 --age-seconds ${PMC_AGE:-20} --no-secondary --no-cpu-baseline --no-parity > $D/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 $D/pmc$i.log; exit 4; }
 done
 python3 scripts/summarize_prof.py $D $TAG $N $DT ${TASK:-hover} > $D/summary.txt
 # profiles/ does not travel back from the box, and the raw traces exceed gpurun_out's 64 MiB: keep the

@@ -16,6 +16,10 @@ SINGLE = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false),
 GENERIC = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), false, false(, (true|false))?>")
 MULTI = re.compile(r"step_kernel<\d+, (true|false), (true|false), (true|false), true, (true|false)(, (true|false))?>")
 
+# KERNEL_RE (environment): summarise the launches of another kernel instead (the re-trim profiles:
+# "retrim_kernel" for same-step auto-reset, "step_ov_kernel" for the overlapped next-step launch)
+if os.environ.get("KERNEL_RE"):
+    SINGLE = re.compile(os.environ["KERNEL_RE"])
 d, tag, n, dt = sys.argv[1], sys.argv[2], int(sys.argv[3]), float(sys.argv[4])
 task = sys.argv[5] if len(sys.argv) > 5 else "hover"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -41,7 +45,9 @@ for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursiv
             gdurs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 mean = {k: sum(v) / len(v) for k, v in agg.items()}
 out = {"tag": tag, "envs": n, "dt": dt, "task": task,
-       "kernel": (", ".join(sorted(names)) or "step_kernel<HOVER, BAKED>") + " (specialised)",
+       "kernel": (", ".join(sorted(names)) or "step_kernel<HOVER, BAKED>")
+       + ("" if os.environ.get("KERNEL_RE") else " (specialised)"),
+       "bench_args": os.environ.get("BENCH_ARGS", ""),
        "kernel_avg_ns_trace": sum(durs) / len(durs) if durs else None,
        "launches_traced": len(durs), "counters_per_launch": mean}
 if gdurs:

@@ -59,6 +59,11 @@ __global__ void __launch_bounds__(64) k(double* out, unsigned long long* cyc, in
         if (K == 20) {   // permlane16 swap chain
             for (int r = 0; r < 16; ++r) { auto t = __builtin_amdgcn_permlane16_swap(u, v, false, false); u = t[0] + 1; v = t[1]; }
         }
+        if (K == 22) asm volatile(S16("s_nop 1\n v_mov_b64_dpp %0, %0 row_newbcast:3 row_mask:0xf bank_mask:0xf\n") : "+v"(a));
+        if (K == 23) asm volatile(S16("v_rcp_f64 %0, %0\n") : "+v"(a));
+        if (K == 24) asm volatile(S16("s_nop 1\n v_fmac_f64_dpp %0, %0, %1 row_newbcast:3 row_mask:0xf bank_mask:0xf\n") : "+v"(a) : "v"(m));
+        if (K == 25) asm volatile(S16("s_nop 1\n v_fma_f64 %0, %0, %1, %2\n") : "+v"(a) : "v"(m), "v"(n));
+        if (K == 26) asm volatile(S16("v_fmac_f64 %0, %0, %1\n") : "+v"(a) : "v"(m));
         if (K == 21) asm volatile(S16("ds_bpermute_b32 %0, %1, %0\n s_waitcnt lgkmcnt(0)\n") : "+v"(u) : "v"(w));
     }
     unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -105,5 +110,10 @@ int main() {
     run<19>("v_mul_f64, 1 dependent chain", 1);
     run<20>("permlane16_swap chain (+add) (per swap)", 1);
     run<21>("ds_bpermute + wait (per round trip)", 1);
+    run<22>("s_nop 1 + v_mov_b64_dpp row_newbcast, dependent (per pair)", 1);
+    run<23>("v_rcp_f64, dependent chain", 1);
+    run<24>("s_nop 1 + v_fmac_f64_dpp row_newbcast, dependent (per pair)", 1);
+    run<25>("s_nop 1 + v_fma_f64, dependent (per pair)", 1);
+    run<26>("v_fmac_f64 (e32), dependent chain", 1);
     return 0;
 }

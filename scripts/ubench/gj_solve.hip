@@ -101,6 +101,31 @@ extern "C" int gj_rcp_check(const double* x, double* err, int n) {
     return 0;
 }
 
+// DPP semantics check: out[l] = {v_mov_b64_dpp row_newbcast:3 of in, v_rcp_f64_dpp row_newbcast:3 of in,
+// v_fmac_f64_dpp acc=in, g=2 row_newbcast:3} for one wave
+__global__ void dpp_kernel(const double* in, double* out) {
+    const int l = threadIdx.x;
+    const double v = in[l];
+    const double b = hgk::gjs_bcast<3>(v);
+    const double r = hgk::gjs_rcp_bcast<3>(v);
+    double acc = v;
+    hgk::gjs_fmac_bcast<3>(acc, 2.0);
+    out[3 * l] = b;
+    out[3 * l + 1] = r;
+    out[3 * l + 2] = acc;
+}
+extern "C" int gj_dpp_check(const double* in, double* out) {
+    double *di, *dout;
+    if (hipMalloc(&di, 8 * 64) || hipMalloc(&dout, 8 * 192)) return -1;
+    (void)hipMemcpy(di, in, 8 * 64, hipMemcpyHostToDevice);
+    hipLaunchKernelGGL(dpp_kernel, dim3(1), dim3(64), 0, 0, di, dout);
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    (void)hipMemcpy(out, dout, 8 * 192, hipMemcpyDeviceToHost);
+    (void)hipFree(di);
+    (void)hipFree(dout);
+    return 0;
+}
+
 extern "C" int gj_solve_stamps(unsigned long long* dst) {
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_gjm_t), sizeof(unsigned long long) * 40) == hipSuccess ? 0 : -1;
 }
