@@ -61,6 +61,9 @@ constexpr int kBlock = 256;
 #ifndef HG_STEP_BLOCK
 #define HG_STEP_BLOCK 64
 #endif
+using hgk::kFusedLine;
+using hgk::kFusedSlot;
+using hgk::kFusedWaveCtrs;
 constexpr int kStepBlock = HG_STEP_BLOCK;   // step kernel block: one or more waves, one state tile each
 static_assert(kTileEnvs == 64, "a state tile is one wave");
 constexpr int kStateCols = HG_STATE_COLS;
@@ -136,6 +139,10 @@ struct StepArgs {
     int32_t ov_active;       // the resets due this step are being trimmed by a concurrent retrim_kernel
                              // (ov mode): their state, but for the step counter, and their observation
                              // rows are that kernel's to write
+    // fused same-step re-trim (step_fused_kernel): records published by device-coherent stores (env
+    // last), the resets deferred as in ov mode (the trim writes all but the step counter)
+    unsigned long long* fused_ctr;   // this launch's fused slot (kFusedSlot ints), or NULL (not fused)
+    int32_t* fused_next;     // the next launch's slot, zeroed by this launch
 };
 
 // Model constants travel as a pointer to a device copy (scalar loads); by value they would take
@@ -492,6 +499,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
         if (a.retrim_slot >= 0 && a.retrim_count) a.retrim_count[a.retrim_slot == 2 ? 0 : a.retrim_slot + 1] = 0;
         if (a.ov_count_next) *a.ov_count_next = 0;
     }
+    if (FEAT && bid == 0 && a.fused_next && tid < kFusedWaveCtrs + 1) a.fused_next[kFusedLine * tid] = 0;
+    if (FEAT && bid == 0 && a.fused_next && tid < 2) a.fused_next[1 + tid] = 0;
     const int nsteps = MULTI ? a.nsteps : 1;
     bool defer_st = false;   // (one step per launch) a deferred reset: the step counter alone is stored
     // the re-trim queue (below): the wave's job mask, the slot counter's old value (leader lane), this
@@ -517,7 +526,20 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
                     rw1 = a.retrim_wind[n + i];
                     rw2 = a.retrim_wind[2 * n + i];
                 }
-                a.retrim_recs[slot] = make_int4((int32_t)i, __float_as_int(rw0), __float_as_int(rw1), __float_as_int(rw2));
+                if (a.fused_ctr) {
+                    // fused: the wind, then env, as device-coherent (agent-scope) stores with a wait for
+                    // the wind's between them -- the trim polls env and then reads the wind the same
+                    // way.  No release: the trim reads nothing else this wave stored (deferred reset),
+                    // so no L2 write-back is needed, and its waits for the record flush no cache.
+                    int* rp = reinterpret_cast<int*>(a.retrim_recs + slot);
+                    __hip_atomic_store(rp + 1, __float_as_int(rw0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(rp + 2, __float_as_int(rw1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(rp + 3, __float_as_int(rw2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(rp, (int)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    a.retrim_recs[slot] = make_int4((int32_t)i, __float_as_int(rw0), __float_as_int(rw1), __float_as_int(rw2));
+                }
             }
         }
     };
@@ -638,9 +660,12 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
 
     // auto-reset (same step, or the step after the end)
     const bool do_reset = P.autoreset && active && ((FEAT && P.autoreset_next) ? pending : done);
-    // a next-step reset whose trim runs concurrently with this step (ov mode): only the step counter
-    // is stored here
-    const bool defer = FEAT && a.ov_active && do_reset;
+    // a reset whose trim runs concurrently with this step -- a next-step reset in ov mode, any reset in
+    // a fused launch: only the step counter is stored here, the trim writes the rest
+#ifndef HG_FUSED_NOTRIM   // diagnostic: 1, a fused launch's trim blocks leave at once and its resets
+#define HG_FUSED_NOTRIM 0   // take the template (the step's own cost in that launch); 2, the trim waves
+#endif                      // wait for their records but trim nothing
+    const bool defer = FEAT && (a.ov_active || (a.fused_ctr && !HG_FUSED_NOTRIM)) && do_reset;
     defer_st = defer;
     if (active) {
         st_lane<kNTS>(a.reward + so + blk0, (uint32_t)tid, pending ? 0.f : rew);
@@ -712,9 +737,24 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     if (FEAT && P.reset_retrim) {
         // the reset template's load (issued at the start) waited for here, not after the atomic
         if constexpr (kRtLate) asm volatile("" ::"v"(tpl));
-        rt_job = do_reset && !defer;
+        rt_job = do_reset && !a.ov_active;
         rt_mask = __ballot(rt_job);
-        if (rt_mask) {
+        if (a.fused_ctr) {
+            // fused: every wave counts itself, so that the trim waves know the queue is complete once
+            // the count reaches the wave count.  A wave with jobs reserves them and counts itself in
+            // one atomic (its jobs in the low word, itself in the high word); a wave without, in one of
+            // kFusedWaveCtrs counters on lines of their own, without waiting for the old value: every
+            // wave on one address serialised the atomics (65 536 envs: the step waves ended 10 to 45 us
+            // into the launch, scripts/fused_probe.py)
+            if (rt_mask) {
+                const int leader = __ffsll((long long)rt_mask) - 1;
+                if (lane == leader)
+                    rt_base = (int)(uint32_t)atomicAdd(a.fused_ctr, (1ull << 32) | (unsigned long long)__popcll(rt_mask));
+            } else if (lane == 0) {
+                int32_t* wc = reinterpret_cast<int32_t*>(a.fused_ctr) + kFusedLine * (1 + (int)(bid % kFusedWaveCtrs));
+                __hip_atomic_fetch_add(wc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if (rt_mask) {
             const int leader = __ffsll((long long)rt_mask) - 1;
             if (lane == leader) rt_base = atomicAdd(a.retrim_count + (a.retrim_slot > 0 ? a.retrim_slot : 0), __popcll(rt_mask));
         }
@@ -886,6 +926,32 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     step_body<TASK, false, true, true, false, BAKED, false>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a,
                                                              (int64_t)blockIdx.x - tb);
 }
+
+// reset_mode RETRIM with same-step auto-reset, lone-wave sizes: one launch holds the step and the trims
+// of the resets it queues.  Its first `tb` blocks are trim waves that claim jobs one at a time and wait
+// (s_sleep polls) for each job's record, which the step wave that queued it publishes at its end; a
+// trim starts as soon as its env's step wave is done instead of after the slowest wave, a launch gap
+// and a retrim_kernel start-up.  The resets are deferred as in ov mode (the step wave stores only the
+// step counter, the trim the rest), so the trim reads nothing the step wave stored but the record, and
+// the hand-over is device-coherent stores and loads -- no release or acquire, whose L2 write-back and
+// invalidate per poll slowed the whole launch (a first version: 65 536 envs 91 us per step against
+// 29 serial).  Every step wave reserves its queue slots in one 64-bit counter that also counts the
+// waves, so the trim waves leave once every wave has reserved and the claims are past the queue (and
+// after a bounded wait in any case).  Bitwise the serial path (tested).
+template <int TASK, bool BAKED>
+__global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2))) void step_fused_kernel(
+    const int32_t* __restrict__ rcount, const int4* __restrict__ rrecs, const hg::TrimSetup* __restrict__ rT,
+    const hg::Params<double>* __restrict__ rP, float* __restrict__ state_p, int64_t n_p, uint64_t seed_p,
+    int64_t envoff_p, ParamArg Pa, const Template<float>* __restrict__ Tp, const StepArgs a, const hgk::RetrimArgs r,
+    int32_t tb) {
+    if ((int32_t)blockIdx.x < tb) {
+        if (HG_FUSED_NOTRIM != 1 && (kStepBlock == 64 || threadIdx.x < 64))
+            hgk::retrim_jobs<true>(r, blockIdx.x, tb, rcount, rrecs, rT, rP, 0);
+        return;
+    }
+    step_body<TASK, false, true, true, false, BAKED, false>(state_p, n_p, seed_p, envoff_p, Pa, Tp, a,
+                                                             (int64_t)blockIdx.x - tb);
+}
 #endif
 
 #ifdef HG_RTC   // step_rtc.hip: the step kernel's code and nothing else
@@ -927,12 +993,14 @@ __global__ __launch_bounds__(64) void clock_stamp_kernel(uint64_t* dst) {
 // hipMemsetAsync: captured into a hipGraph, a 4-byte memset node left the counter non-zero on later
 // replays on MI355X (0x08080808 and stale counts in scripts/r04_retrim_fault.py), so the re-trim
 // read a job count past the records its step wrote; a kernel node keeps its arguments by value.
-__global__ __launch_bounds__(64) void zero_counts_kernel(int32_t* a, int32_t* b, int32_t* c) {
+__global__ __launch_bounds__(64) void zero_counts_kernel(int32_t* a, int32_t* b, int32_t* c, int32_t* d) {
     if (threadIdx.x == 0) {
         if (a) *a = 0;
         if (b) *b = 0;
         if (c) *c = 0;
     }
+    if (d && threadIdx.x < kFusedWaveCtrs + 1) d[kFusedLine * threadIdx.x] = 0;   // a fused launch's slot
+    if (d && threadIdx.x < 2) d[1 + threadIdx.x] = 0;
 }
 
 // The rotor azimuths (psi_mr, psi_tr): their rates are the constants Omega (helicopter_dynamics.py:
@@ -1429,6 +1497,7 @@ struct hg_env {
     int4* retrim_recs = nullptr;            // a step's auto-reset jobs {env, wind}
     int32_t* retrim_count = nullptr;        // [0] jobs of hg_reset's re-trim, [1] failures so far, [2] invalid jobs,
                                             // [3] solves tried with the given pivot order, [4] of them rejected
+    int32_t* fused_ring = nullptr;          // [3][kFusedSlot] a fused same-step launch's counters, by the same slot
     int32_t* retrim_ring = nullptr;         // [3] jobs of a step's re-trim: step k counts into [k % 3] and
     uint64_t retrim_gen = 0;                //     zeroes [(k + 1) % 3] from its kernel (no memset launch)
     uint64_t retrim_chain = kChainBroken;   // chain key of the previous re-trim step (see chain_key)
@@ -1438,6 +1507,7 @@ struct hg_env {
     // their step counter (the trims write the rest, and their observation rows).
     bool ov = false;                        // configured (RETRIM + next-step auto-reset) and enabled
     bool ov_enabled = true;                 // hg_set_retrim_overlap
+    bool fused_enabled = false;             // hg_set_retrim_overlap(2): the fused same-step launch
     uint64_t ov_chain = kChainBroken;       // chain key of the previous step when its ends can be trimmed
                                             // concurrently with this one (no other call in between)
     int4* ov_recs = nullptr;                // [3][N] jobs {env, trim wind}
@@ -1549,9 +1619,10 @@ static int32_t build_template(hg_env* e) {
     return HG_OK;
 }
 
-static hipError_t zero_counts(int32_t* const p[3], hipStream_t s) {
-    if (!p[0] && !p[1] && !p[2]) return hipSuccess;
-    hipLaunchKernelGGL(zero_counts_kernel, dim3(1), dim3(64), 0, s, p[0], p[1], p[2]);
+// pair (optional): a fused launch's {jobs, waves, claim}
+static hipError_t zero_counts(int32_t* const p[3], hipStream_t s, int32_t* pair = nullptr) {
+    if (!p[0] && !p[1] && !p[2] && !pair) return hipSuccess;
+    hipLaunchKernelGGL(zero_counts_kernel, dim3(1), dim3(64), 0, s, p[0], p[1], p[2], pair);
     return hipGetLastError();
 }
 
@@ -1664,6 +1735,20 @@ static void launch_step_ov(const hg_env* e, hipStream_t s, const StepArgs& a, co
     }
 }
 
+static void launch_step_fused(const hg_env* e, hipStream_t s, const StepArgs& a, const hgk::RetrimArgs& r, int32_t tb) {
+    const unsigned grid = (unsigned)((e->n + kStepBlock - 1) / kStepBlock) + (unsigned)tb;
+    auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kStepBlock), 0, s, r.count, r.recs, r.T, r.P, STEP_KARGS(e), a, r, tb);
+    };
+    switch (e->cfg.task) {
+        case HG_TASK_HOVER: e->baked ? go(step_fused_kernel<HG_TASK_HOVER, true>) : go(step_fused_kernel<HG_TASK_HOVER, false>); break;
+        case HG_TASK_FORWARD_FLIGHT:
+            e->baked ? go(step_fused_kernel<HG_TASK_FORWARD_FLIGHT, true>) : go(step_fused_kernel<HG_TASK_FORWARD_FLIGHT, false>);
+            break;
+        default: e->baked ? go(step_fused_kernel<HG_TASK_HELI, true>) : go(step_fused_kernel<HG_TASK_HELI, false>); break;
+    }
+}
+
 extern "C" {
 #if HG_TIMING
 int hg_debug_timing(void* dst, int64_t bytes) {
@@ -1671,6 +1756,9 @@ int hg_debug_timing(void* dst, int64_t bytes) {
 }
 int hg_debug_timing_help(void* dst, int64_t bytes) {
     return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_timing_help), (size_t)bytes) == hipSuccess ? 0 : -1;
+}
+int hg_debug_fused_probe(void* dst, int64_t bytes) {
+    return hipMemcpyFromSymbol(dst, HIP_SYMBOL(hgk::g_fused_probe), (size_t)bytes) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -1769,7 +1857,7 @@ static void release(hg_env* e) {
     }
     dfree(e->hmap); dfree(e->state); dfree(e->az); dfree(e->tmpl_dev); dfree(e->params_dev);
     dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_recs);
-    dfree(e->retrim_count); dfree(e->retrim_ring); dfree(e->ov_recs); dfree(e->ov_ring);
+    dfree(e->retrim_count); dfree(e->retrim_ring); dfree(e->ov_recs); dfree(e->ov_ring); dfree(e->fused_ring);
     dfree(e->tmpl_env); dfree(e->setup_batch);
     delete e;
 }
@@ -1862,6 +1950,8 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if ((err = hipMemset(e->retrim_count, 0, 5 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim");
     if ((err = hipMalloc(&e->retrim_ring, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim ring");
     if ((err = hipMemset(e->retrim_ring, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim ring");
+    if ((err = hipMalloc(&e->fused_ring, 3 * kFusedSlot * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc fused ring");
+    if ((err = hipMemset(e->fused_ring, 0, 3 * kFusedSlot * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset fused ring");
     if (cfg->reset_mode == HG_RESET_RETRIM) {
         if ((err = hipMalloc(&e->retrim_wind, sizeof(float) * 3 * num_envs)) != hipSuccess)
             return cleanup(err, "hipMalloc retrim wind");
@@ -2069,6 +2159,10 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     // noise and the library's own kernels; otherwise this step's due resets take the serial re-trim
     const bool ov_active = ov && e->ov_chain == key && !eager_after_capture && !eta && !e->rtc &&
                            e->n <= HG_NT_WAVES * e->resident_envs;
+    // fused same-step re-trim (step_fused_kernel, opt-in: hg_set_retrim_overlap(2)): the step's resets
+    // trimmed in its own launch, for the lone-wave sizes, in-kernel noise and the library's own kernels
+    const bool fused = retrim && !e->ov && e->fused_enabled && !eta && !e->rtc && e->n <= HG_NT_WAVES * e->resident_envs;
+    int32_t* fused_pair = nullptr;
     if (retrim) {   // the step's re-trim job count: a slot of the ring, zeroed by the previous step's kernel
         rt_slot = (int32_t)(e->retrim_gen % 3);
         rt_count = e->retrim_ring + rt_slot;
@@ -2076,10 +2170,11 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         if (e->retrim_chain != key || eager_after_capture) {
             zero[1] = rt_count;
             if (ov) zero[2] = e->ov_ring + rt_slot;
+            if (fused) fused_pair = e->fused_ring + kFusedSlot * rt_slot;
         }
         e->retrim_chain = key;
     }
-    HIP_TRY(zero_counts(zero, s));
+    HIP_TRY(zero_counts(zero, s, fused_pair));
     StepArgs a;
     a.hmap = e->hmap;
     a.actions = actions;
@@ -2104,6 +2199,8 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
     a.ov_count = ov ? e->ov_ring + rt_slot : nullptr;
     a.ov_count_next = ov ? e->ov_ring + (rt_slot == 2 ? 0 : rt_slot + 1) : nullptr;
     a.ov_active = ov_active ? 1 : 0;
+    a.fused_ctr = fused ? reinterpret_cast<unsigned long long*>(e->fused_ring + kFusedSlot * rt_slot) : nullptr;
+    a.fused_next = fused ? e->fused_ring + kFusedSlot * (rt_slot == 2 ? 0 : rt_slot + 1) : nullptr;
     const bool feat = reset_count || e->Pf.reset_retrim || e->Pf.autoreset_next ||
                       e->Pf.max_episode_steps != INT32_MAX || e->Pf.env_templates;
     ++e->n_launch[0];
@@ -2127,12 +2224,37 @@ static int32_t step_impl(hg_env* e, const float* actions, float* obs, float* rew
         r.tmpl = reinterpret_cast<const float*>(e->tmpl_dev);
         r.tmpl_env = e->Pf.env_templates ? e->tmpl_env : nullptr;
         launch_step_ov(e, s, a, r);
+    } else if (fused) {   // this step's resets trimmed in its own launch's first blocks
+        ++e->n_launch[1];
+#ifndef HG_FUSED_TB_DIV
+#define HG_FUSED_TB_DIV 1
+#endif
+        const int32_t tb = ov_trim_blocks(e->n) / HG_FUSED_TB_DIV;
+        hgk::RetrimArgs r;
+        memset(&r, 0, sizeof(r));
+        r.P = e->pd_dev;
+        r.T = e->setup_dev;
+        r.recs = e->retrim_recs;   // (no count: the queue's end is r.ctr's low word once every wave reserved)
+        r.state = e->state;
+        r.az = e->az;
+        r.obs = obs;
+        r.n = e->n;
+        r.fail_count = e->retrim_count + 1;
+        r.bad_jobs = e->retrim_count + 2;
+        r.solve_stats = e->retrim_count + 3;
+        r.ov = 1;   // the deferred resets: the trim writes all but the step counter
+        r.tmpl = reinterpret_cast<const float*>(e->tmpl_dev);
+        r.tmpl_env = e->Pf.env_templates ? e->tmpl_env : nullptr;
+        r.claim = e->fused_ring + kFusedSlot * rt_slot + 2;
+        r.ctr = reinterpret_cast<const unsigned long long*>(e->fused_ring + kFusedSlot * rt_slot);
+        r.nwaves = (int32_t)((e->n + kStepBlock - 1) / kStepBlock);
+        launch_step_fused(e, s, a, r, tb);
     } else {
         HIP_TRY(dispatch_task<false>(e, s, a, eta != nullptr, feat));
     }
     HIP_TRY(hipGetLastError());
     if (ov) e->ov_chain = key;
-    if (retrim && !ov_active) {   // re-trim this step's resets against their last wind (overwrites the template)
+    if (retrim && !ov_active && !fused) {   // re-trim this step's resets against their last wind (overwrites the template)
         hgk::RetrimArgs r;
         memset(&r, 0, sizeof(r));
         r.P = e->pd_dev;
@@ -2365,7 +2487,9 @@ int32_t hg_debug_launches(const hg_env* e, int64_t* out) {
 
 int32_t hg_set_retrim_overlap(hg_env* e, int32_t enable) {
     if (!e) return fail(HG_E_INVALID, "env is NULL");
+    if (enable < 0 || enable > 2) return fail(HG_E_INVALID, "hg_set_retrim_overlap: enable is 0, 1 or 2");
     e->ov_enabled = enable != 0;
+    e->fused_enabled = enable == 2;
     e->ov_chain = kChainBroken;
     return (e->ov && e->ov_enabled) ? 1 : 0;
 }

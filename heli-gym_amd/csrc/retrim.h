@@ -53,6 +53,13 @@ struct AzRec {
 __host__ __device__ inline int32_t episode_steps(int32_t step) { return step >= 0 ? step : -(step + 1); }
 inline int64_t tile_words(int64_t n) { return ((n + kTileEnvs - 1) / kTileEnvs) * kTileWords; }
 
+// a fused same-step launch's counters (one slot of a ring of three): ints [0, 1] the 64-bit {queued jobs,
+// waves with jobs}, [2] the trim waves' claim counter, then kFusedWaveCtrs counters of the waves without
+// jobs, each at the start of a 64-byte line of its own (kFusedLine ints)
+constexpr int kFusedLine = 16;
+constexpr int kFusedWaveCtrs = 16;
+constexpr int kFusedSlot = kFusedLine * (kFusedWaveCtrs + 1);
+
 struct RetrimArgs {
     const hg::Params<double>* P;
     const hg::TrimSetup* T;
@@ -81,6 +88,13 @@ struct RetrimArgs {
     int32_t* bad_jobs;      // env mode: job records naming no env (or a count past N), skipped and counted
     int32_t* solve_stats;   // [0] Newton solves tried with the setup's pivot order, [1] of them rejected
                             // by the residual test (and searched instead); may be NULL
+    // fused same-step mode (step_fused_kernel): the trims run in the step's own launch and take each
+    // job as soon as the step wave that queued it has published its record (device-coherent stores,
+    // env last); claim hands out job indices; ctr is the launch's slot (kFusedSlot ints): the queue is
+    // complete once every step wave has counted itself
+    int32_t* claim;         // NULL: not fused
+    const unsigned long long* ctr;
+    int32_t nwaves;         // step waves of the launch
 };
 
 // Launch retrim_kernel (one 64-lane block per trim, up to `grid` blocks looping over the jobs).

@@ -26,6 +26,14 @@ __device__ unsigned long long g_rt_timing[64];
 #else
 #define RSTAMP(j, ...) do { } while (0)
 #endif
+#if HG_TIMING
+// diagnostic build: a fused launch's trim waves, per job (< 1024): s_memrealtime at the claim, at the
+// record's arrival and at the write-out
+__device__ unsigned long long g_fused_probe[1024][4];
+#define FSTAMP(k) do { if (FUSED && l == 0 && job < 1024) g_fused_probe[job][(k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define FSTAMP(k) do { } while (0)
+#endif
 
 __device__ __forceinline__ double read_lane(double v, int lane) {
     const uint64_t u = __double_as_longlong(v);
@@ -381,6 +389,15 @@ __device__ unsigned g_rt_dbg_n;
 // and Tstride_p = a.setup_stride: the job count, the first record, the first job's setup and a
 // prefetch of the model constants are all requested at once, before the kernel-argument segment has
 // arrived (round 6: each was a dependent memory round trip of the trim's start-up).
+#ifndef HG_FUSED_MAX_POLLS   // a fused trim wave waits at most this many polls for a record (never reached)
+#define HG_FUSED_MAX_POLLS (1 << 20)
+#endif
+#ifndef HG_FUSED_SLEEP       // s_sleep between a fused trim wave's polls (units of 64 clocks)
+#define HG_FUSED_SLEEP 4
+#endif
+// FUSED (step_fused_kernel): jobs are claimed one at a time (a.claim) and each record waited for until
+// its step wave publishes it, or until every step wave has reserved and the claim is past the queue.
+template <bool FUSED = false>
 __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, int64_t stride, const int32_t* count_p,
                                             const int4* recs_p, const hg::TrimSetup* T_p, const hg::Params<double>* P_p,
                                             int32_t Tstride_p) {
@@ -418,7 +435,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     // (a launch has at most one block per env, so recs_p[first] is a record; with no queue, no load)
     int4 rec0_v = make_int4(-1, 0, 0, 0);
     int32_t count_v = 0;
-    if (recs_p || count_p) {
+    if (!FUSED && (recs_p || count_p)) {
         const int32_t* any = count_p ? count_p : reinterpret_cast<const int32_t*>(recs_p);
         rec0_v = (recs_p ? recs_p + first : reinterpret_cast<const int4*>(any))[zero_v];
         count_v = any[zero_v];
@@ -457,15 +474,68 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
         if (first == 0 && l == 0 && a.bad_jobs) atomicAdd(a.bad_jobs, 1);
         jobs = a.n;
     }
-    for (int64_t job = first; job < jobs; job += stride) {   // uniform per wave
-        const int4 rec = a.recs ? (job == first ? rec0 : a.recs[job]) : make_int4(0, 0, 0, 0);
+    for (int64_t job = first; FUSED || job < jobs; job += stride) {   // uniform per wave
+        int4 rec;
+        if constexpr (FUSED) {
+            // claim the next job, then wait for its record (env >= 0, stored last) or for the end: every
+            // step wave reserved and the claim past the queue.  Device-coherent loads only (no acquire,
+            // whose L2 invalidate per poll would evict the step waves' data); the wind is read after
+            // env, as the step wave stored it before env.
+            int claimed = 0;
+            if (l == 0) claimed = atomicAdd(a.claim, 1);
+            job = __builtin_amdgcn_readfirstlane(claimed);
+            if (job >= a.n) break;
+            FSTAMP(0);
+            int* rp = reinterpret_cast<int*>(const_cast<int4*>(a.recs) + job);
+            int x = -1;
+            bool end = false;
+            for (int polls = 0; x < 0 && !end; ++polls) {
+                x = __builtin_amdgcn_readfirstlane(__hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                if (x < 0) {
+                    // {queued jobs, waves with jobs}, and lanes 0..15 the counts of waves without
+                    const unsigned long long q =
+                        __hip_atomic_load(const_cast<unsigned long long*>(a.ctr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    int wl = 0;
+                    if (l < kFusedWaveCtrs)
+                        wl = __hip_atomic_load(reinterpret_cast<const int32_t*>(a.ctr) + kFusedLine * (1 + l), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                    const int qn = __builtin_amdgcn_readfirstlane((int)(uint32_t)q);
+                    int wn = __builtin_amdgcn_readfirstlane((int)(uint32_t)(q >> 32));
+#pragma unroll
+                    for (int k = 0; k < kFusedWaveCtrs; ++k) wn += __builtin_amdgcn_readlane(wl, k);
+                    // (each count is bounded by its own waves, so the parts read at different times
+                    // reach the wave count only once every wave with jobs has reserved: qn is final)
+                    end = wn >= a.nwaves && job >= qn;
+                    if (!end && polls >= HG_FUSED_MAX_POLLS) {   // (a step wave that never reserved)
+                        if (l == 0 && a.bad_jobs) atomicAdd(a.bad_jobs, 1);
+                        end = true;
+                    }
+                    if (!end) __builtin_amdgcn_s_sleep(HG_FUSED_SLEEP);
+                }
+            }
+            if (x < 0) break;
+            FSTAMP(1);
+            asm volatile("" ::: "memory");
+            rec = make_int4(x, __builtin_amdgcn_readfirstlane(__hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                            __builtin_amdgcn_readfirstlane(__hip_atomic_load(rp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                            __builtin_amdgcn_readfirstlane(__hip_atomic_load(rp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+            if (l == 0) rp[0] = -1;   // the slot free for the next launch's queue
+#if defined(HG_FUSED_NOTRIM) && HG_FUSED_NOTRIM == 2
+            continue;
+#endif
+        } else {
+            rec = a.recs ? (job == first ? rec0 : a.recs[job]) : make_int4(0, 0, 0, 0);
+            // every consumed record goes back to env -1, so that a fused launch (which waits for env >= 0)
+            // never takes a record an earlier launch of the other paths left behind
+            if (a.recs && l == 0) const_cast<int4*>(a.recs)[job].x = -1;
+        }
         const int64_t env = a.recs ? (int64_t)rec.x : (a.list ? (int64_t)a.list[job] : job);
         if ((a.recs || a.list) && (uint64_t)env >= (uint64_t)a.n) {   // never index the state with a bad record
             if (l == 0 && a.bad_jobs) atomicAdd(a.bad_jobs, 1);
             continue;
         }
         const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];
-        const bool j0 = job == first;   // (its setup requested at entry)
+        const bool j0 = job == first || !Tstride_p;   // (its setup requested at entry: every job's, with one setup)
 #if HG_GJ_MFMA && HG_GJ_STATIC
         const int8_t piv_v = j0 ? piv_l : T.piv[l >> 4][l & 15];
         sPiv[l] = piv_v;
@@ -702,6 +772,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             if (a.out_status) a.out_status[job] = HG_E_TRIM;
         }
         RSTAMP(61, "v"(l));   // the write-out issued
+        FSTAMP(2);
         lds_order();   // the next job's writes come after this job's reads
     }
     if (pf == 0x7FC00001u && jobs == -12345 && a.bad_jobs) atomicAdd(a.bad_jobs, 0);   // (keeps the prefetch)

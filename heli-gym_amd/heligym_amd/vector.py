@@ -430,10 +430,13 @@ class HeliVecEnv(*_VEC_BASES):
         return self._specialized
 
     def set_retrim_overlap(self, enable=True):
-        """reset_mode="retrim" with next-step auto-reset: trim the episodes a step ends while the next
-        step runs (hg_set_retrim_overlap; the default, bitwise the serial results).  Returns whether
-        the overlap is in effect."""
-        rc = self.lib.hg_set_retrim_overlap(self._h, 1 if enable else 0)
+        """reset_mode="retrim": with next-step auto-reset, trim the episodes a step ends while the next
+        step runs (True, the default; False: always serial).  enable=2 also trims, with same-step
+        auto-reset, a step's resets in the step's own launch as soon as each env's step is done (opt-in:
+        bitwise the serial results but slower on MI355X).  hg_set_retrim_overlap.  Returns whether the
+        next-step overlap is in effect."""
+        mode = 2 if (enable == 2 and enable is not True) else (1 if enable else 0)
+        rc = self.lib.hg_set_retrim_overlap(self._h, mode)
         if rc < 0:
             self._check(rc)
         return bool(rc)

@@ -322,8 +322,12 @@ int32_t hg_debug_launches(const hg_env* env, int64_t* out);
  * step's ends only when that step was the previous launch of the same sequence (eager, or captured
  * into the same graph) with no other state-changing call on the handle in between, with in-kernel
  * noise and at most two step waves per SIMD (N <= 131 072 on MI355X); otherwise its due resets are
- * trimmed after it, serially.  enable = 1 (the default) or 0 (always serial: A/B and tests).
- * Returns 1 if the mode is configured and enabled, 0 otherwise, or HG_E_*. */
+ * trimmed after it, serially.  enable = 1 (the default) or 0 (always serial: A/B and tests); 2 also
+ * fuses, with same-step auto-reset, a step's re-trims into its own launch: trim blocks first, each
+ * taking a reset as soon as its env's step wave has published it (in-kernel noise, at most two step
+ * waves per SIMD).  Bitwise the serial path, but slower on MI355X (65 536 envs: 33.7 against 29.4 us
+ * per step; the step waves run about 7 us longer beside the trims), so opt-in.  Returns 1 if the
+ * next-step mode is configured and enabled, 0 otherwise, or HG_E_*. */
 int32_t hg_set_retrim_overlap(hg_env* env, int32_t enable);
 
 /* State access for parity tests / checkpointing (the reference's StateNumpy,

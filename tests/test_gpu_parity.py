@@ -1029,15 +1029,16 @@ def test_next_step_autoreset(torch):
     assert checked > N // 2, checked
 
 
-def _retrim_next_step_run(torch, N, K, overlap, graph_steps=0, seed=13):
+def _retrim_next_step_run(torch, N, K, overlap, graph_steps=0, seed=13, amode="next_step"):
     """reset_mode="retrim" + next-step auto-reset, half the envs crashing (low collective): per-step
     obs, reward, flags and info, plus the state and counters read mid-run and at the end.  Eager, a
     get_state() at step 100 and a masked reset() at step 150 (each breaks the overlap chain once); or,
     with graph_steps, hipGraphs of that many steps (each recording its outputs) replayed back to back
     with one eager step between two replays."""
-    env = make_env(torch, N, "hover", 0.02, autoreset=True, reset_mode="retrim", autoreset_mode="next_step",
+    env = make_env(torch, N, "hover", 0.02, autoreset=True, reset_mode="retrim", autoreset_mode=amode,
                    seed=seed)
-    assert env.set_retrim_overlap(overlap) == overlap
+    ov = env.set_retrim_overlap(overlap)
+    assert ov == (bool(overlap) and amode == "next_step")
     env.reset()
     acts = torch.empty((K, N, 4), dtype=torch.float32, device=env.device)
     for k in range(K):
@@ -1111,6 +1112,29 @@ def test_retrim_overlap_bitwise_equals_serial(torch, N, graph_steps):
     assert b0 == b1 == 0
     assert f0 == f1
     for j, (x, y) in enumerate(zip(serial, over)):
+        np.testing.assert_array_equal(x, y, err_msg=f"output {j}")
+
+
+@pytest.mark.parametrize("N,graph_steps", [(1000, 0), (1000, 40), (16, 0), (65536, 0)])
+def test_retrim_fused_same_step_bitwise_equals_serial(torch, N, graph_steps):
+    """reset_mode="retrim" with same-step auto-reset: the step's resets are re-trimmed in the step's
+    own launch (step_fused_kernel: trim waves that take each job as soon as its step wave has
+    published it), and the results -- observations, rewards, flags, state, counters -- are bitwise
+    those of the serial path (the step, then retrim_kernel), eager (with a get_state and a masked reset
+    between steps) and graph-replayed.  The fused launches are counted (hg_debug_launches), so the
+    comparison cannot pass with both runs serial; no job record is skipped as invalid and no trim
+    wave gives up waiting (hg_debug_retrim_invalid).  N = 65 536: the bench's size, many resets per
+    launch spread over the trim waves."""
+    K = 250 if not graph_steps else 243
+    serial, f0, l0, b0 = _retrim_next_step_run(torch, N, K, False, graph_steps, amode="same_step")
+    fused, f1, l1, b1 = _retrim_next_step_run(torch, N, K, 2, graph_steps, amode="same_step")
+    ends = int((serial[2] | serial[3]).sum())
+    assert ends > (200 if N >= 1000 else 4), ends
+    assert l0["overlapped_retrim"] == 0
+    assert l1["overlapped_retrim"] >= K - 2, l1
+    assert b0 == b1 == 0
+    assert f0 == f1
+    for j, (x, y) in enumerate(zip(serial, fused)):
         np.testing.assert_array_equal(x, y, err_msg=f"output {j}")
 
 
