@@ -198,11 +198,25 @@ def cpu_share():
 
 
 # ------------------------------------------------------------------------------------ references
-def pmc_summary(envs, dt, task, need="hbm_bytes_per_launch", tags=None):
+def summary_mode(d):
+    """The reset path a PMC summary profiled, from the bench options it was run with (its
+    `bench_args`): ("template", "same_step") for the step kernel's own profiles, ("retrim", amode) for
+    the re-trim ones (retrim_kernel / step_ov_kernel).  The auto-reset mode only matters with re-trim."""
+    tok = (d.get("bench_args") or "").split()
+    opt = lambda k, dflt: tok[tok.index(k) + 1] if k in tok and tok.index(k) + 1 < len(tok) else dflt
+    rm = opt("--reset-mode", "template")
+    return (rm, opt("--autoreset-mode", "same_step") if rm == "retrim" else "same_step")
+
+
+def pmc_summary(envs, dt, task, need="hbm_bytes_per_launch", tags=None, mode=("template", "same_step")):
     """The newest committed PMC summary for this workload (profiles/<tag>_pmc_summary.json, written
     by scripts/summarize_prof.py from rocprofv3 --pmc passes) that has `need`, as (dict, path), or
-    None.  Newest = last in tag order; `tags` restricts the search to those tags."""
+    None.  Newest = last in tag order; `tags` restricts the search to those tags.  The summary must
+    be of the same reset path (`mode` = (reset_mode, autoreset_mode), summary_mode), so a re-trim
+    line never carries the template step kernel's counters or the other way round."""
     import glob
+    if mode[0] != "retrim":
+        mode = ("template", "same_step")
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
         try:
@@ -212,7 +226,8 @@ def pmc_summary(envs, dt, task, need="hbm_bytes_per_launch", tags=None):
         if tags is not None and d.get("tag") not in tags:
             continue
         have = need in d or need in d.get("counters_per_launch", {})
-        if d.get("envs") == envs and abs(d.get("dt", -1) - dt) < 1e-12 and d.get("task", "hover") == task and have:
+        if (d.get("envs") == envs and abs(d.get("dt", -1) - dt) < 1e-12 and d.get("task", "hover") == task and have
+                and summary_mode(d) == tuple(mode)):
             best = (d, os.path.relpath(f, ROOT))
     return best
 
@@ -229,9 +244,9 @@ def pattern_ceiling():
         return None
 
 
-def pmc_traffic(envs, dt, task):
-    """HBM bytes per step-kernel launch (FETCH_SIZE / WRITE_SIZE passes), or None."""
-    r = pmc_summary(envs, dt, task)
+def pmc_traffic(envs, dt, task, mode=("template", "same_step")):
+    """HBM bytes per launch of the reset path's profiled kernel (FETCH_SIZE / WRITE_SIZE passes), or None."""
+    r = pmc_summary(envs, dt, task, mode=mode)
     return None if r is None else (r[0]["hbm_bytes_per_launch"], r[1])
 
 
@@ -245,11 +260,11 @@ def shader_clock_ghz(dt, task, fallback_ghz):
     return fallback_ghz, "device maximum clock"
 
 
-def valu_issue(envs, dt, task, kern_s, simds, clock_ghz):
+def valu_issue(envs, dt, task, kern_s, simds, clock_ghz, mode=("template", "same_step")):
     """The VALU issue ceiling beside the HBM one: VALU wave-instructions per
     launch (SQ_INSTS_VALU of the committed PMC summary of this workload) x 4 cycles (a wave issues at
     most one VALU instruction per ~4 cycles) / (SIMDs x clock x the live per-launch time)."""
-    r = pmc_summary(envs, dt, task, need="SQ_INSTS_VALU")
+    r = pmc_summary(envs, dt, task, need="SQ_INSTS_VALU", mode=mode)
     if r is None:
         return None
     c = r[0]["counters_per_launch"]
@@ -1133,6 +1148,7 @@ def main():
                      "impl_bytes_per_env_step": IMPL_BYTES_PER_ENV_STEP,
                      "algorithmic_bytes_per_launch": (total_envs // world) * BYTES_PER_ENV_STEP},
     }
+    head_mode = (args.reset_mode, args.autoreset_mode)   # the reset path whose PMC summary applies
     if args.dry_run:
         out["dry_run"] = "plumbing check only: no kernel ran, nothing was measured"
         out["roofline"].update(achieved=None, frac=None)
@@ -1140,7 +1156,7 @@ def main():
         props = torch.cuda.get_device_properties(dev)
         simds = 4 * props.multi_processor_count
         ghz, ghz_src = shader_clock_ghz(args.dt, args.task, getattr(props, "clock_rate", 2400000) / 1e6)
-        vi = valu_issue(total_envs // world, args.dt, args.task, kern_s, simds, ghz)
+        vi = valu_issue(total_envs // world, args.dt, args.task, kern_s, simds, ghz, mode=head_mode)
         if vi is not None:
             out["roofline"].update(vi, clock_ghz=ghz, clock_source=ghz_src)
         if "out_of_cache" in secondary:
@@ -1151,7 +1167,7 @@ def main():
     if args.gather_obs:
         out["roofline"]["kernel_avg_source"] = "timed window / steps (eager with gathers: an upper bound)"
     out.update(secondary)
-    tr = None if args.dry_run else pmc_traffic(total_envs // world, args.dt, args.task)
+    tr = None if args.dry_run else pmc_traffic(total_envs // world, args.dt, args.task, mode=head_mode)
     if tr is not None:
         out["roofline"]["traffic"] = tr[0]
         out["roofline"]["traffic_source"] = tr[1] + " (HBM bytes per launch, PMC)"

@@ -38,7 +38,7 @@ for f in glob.glob(os.path.join(d, "trace", "**", "*kernel_trace.csv"), recursiv
     for r in csv.DictReader(open(f)):
         if SINGLE.search(r["Kernel_Name"]):
             durs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-            names.add(r["Kernel_Name"].split("(")[0].replace("(anonymous namespace)::", ""))
+            names.add(r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "", 1).split("(")[0])
         elif MULTI.search(r["Kernel_Name"]):
             mdurs.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         elif GENERIC.search(r["Kernel_Name"]):
@@ -67,8 +67,9 @@ if "FETCH_SIZE" in mean and "WRITE_SIZE" in mean:
     out["traffic_note"] = ("2*FETCH_SIZE + WRITE_SIZE (KiB*1024), the gfx950 FETCH_SIZE x2 correction, checked for "
                            "this kernel's 4-B and 16-B-per-lane accesses on known byte counts in "
                            "profiles/*_pmc_calibration.json")
-    out["impl_bytes_per_launch"] = n * (128 + 187)   # bench.py IMPL_BYTES_PER_ENV_STEP
-    out["algorithmic_bytes_per_launch"] = n * 318
+    if not os.environ.get("KERNEL_RE"):   # (the step kernel's byte model; a trim kernel has none)
+        out["impl_bytes_per_launch"] = n * (128 + 187)   # bench.py IMPL_BYTES_PER_ENV_STEP
+        out["algorithmic_bytes_per_launch"] = n * 318
 with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as f:
     json.dump(out, f, indent=1)
 print(json.dumps(out, indent=1))

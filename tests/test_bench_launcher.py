@@ -93,3 +93,24 @@ def test_world_size_mismatch_fails():
 def test_gather_obs_needs_ranks():
     rc, lines, err = run("--gather-obs")
     assert rc != 0 and not lines
+
+
+def test_pmc_summary_is_keyed_on_the_reset_path(tmp_path, monkeypatch):
+    """pmc_summary() only returns a summary of the same reset path: a re-trim line (retrim_kernel or
+    step_ov_kernel profiles) never carries the template step kernel's counters, nor the other way round
+    (the sweep's re-trim lines showed the template kernel's VALU and traffic)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    base = {"envs": 65536, "dt": 0.01, "task": "hover", "hbm_bytes_per_launch": 1.0}
+    for tag, args in (("a1", ""), ("a2", "--reset-mode retrim --autoreset-mode same_step"),
+                      ("a3", "--reset-mode retrim --autoreset-mode next_step")):
+        (prof / f"{tag}_pmc_summary.json").write_text(json.dumps({**base, "tag": tag, "bench_args": args}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    got = lambda mode: bench.pmc_summary(65536, 0.01, "hover", mode=mode)[0]["tag"]
+    assert got(("template", "same_step")) == "a1"
+    assert got(("template", "next_step")) == "a1"   # (the auto-reset mode only matters with re-trim)
+    assert got(("retrim", "same_step")) == "a2"
+    assert got(("retrim", "next_step")) == "a3"
+    assert bench.pmc_summary(65536, 0.01, "hover", mode=("retrim", "same_step"), tags=["a1"]) is None
