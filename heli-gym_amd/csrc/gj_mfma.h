@@ -198,11 +198,12 @@ __device__ __forceinline__ void gjm_solve(const double* sE, int es, double s, in
 // is the pivot's reciprocal (one Newton step), the multipliers, and one fused update per element.
 // Its dependent chain is five instructions.
 //   * Rows stay unscaled (the pivot row's multiplier is 0); x[C] = b[C] / pivot at the end.
-//   * The augmented columns are one register: quarter q carries column q of Aug = E[:, P] (the
-//     lazily injected identity column e_{4p+q} from the panel's start), and one v_fmac_f64_dpp per
-//     step updates all four quarters -- the broadcast from lane C of each quarter is exactly the pivot
-//     row's entry of that quarter's column.  The MFMAs then take C with the panel's pivot rows zeroed:
-//     (J - S S^T J) + Aug S^T J = E J.
+//   * The augmented columns are one register: quarter q carries column q of Aug - S, Aug = E[:, P]
+//     (the lazily injected identity column e_{4p+q} from the panel's start) less that identity column,
+//     and one v_fmac_f64_dpp per step updates all four quarters -- the broadcast from lane C of each
+//     quarter is the pivot row's entry of that quarter's column -- plus the identity's share in
+//     quarter K.  The MFMAs then take the system itself as C: J + (Aug - S) S^T J = E J (no selects
+//     zeroing the pivot rows on the chain).
 //   * The next panel's columns come out of a second MFMA already replicated over the quarters (the
 //     rows of its A operand repeat each pivot row's entry of those columns), and every LDS address a
 //     panel needs is known before its pivots are: no lane shuffle and no LDS wait on the step chain.
@@ -255,8 +256,9 @@ __device__ __forceinline__ double gjs_quarter_sum(double x) {   // sum over the 
 }
 
 template <int PN, int K>
-__device__ __forceinline__ void gjs_step(double (&c)[4], double& bop, double& myinv, int i) {
+__device__ __forceinline__ void gjs_step(double (&c)[4], double& bop, double& myinv, int i, int q) {
     constexpr int C = 4 * PN + K;
+    const double cz = c[K] * (i == C ? 0.0 : 1.0);   // (off the chain) the pivot row is not updated
     const double p = K == 0 ? gjs_bcast_c<C>(c[K]) : gjs_bcast<C>(c[K]);   // the pivot J[C][C]
 #if GJS_RCP_DPP
     double r = gjs_rcp_bcast<C>(c[K]);
@@ -264,12 +266,18 @@ __device__ __forceinline__ void gjs_step(double (&c)[4], double& bop, double& my
     double r = __builtin_amdgcn_rcp(p);
 #endif
     r = fma(r, fma(-p, r, 1.0), r);                  // one Newton step: within 1e-14 (the residual test guards)
-    const double cz = i == C ? 0.0 : c[K];           // (off the chain) the pivot row is not updated
     const double g = -cz * r;                        // -J[i][C] / pivot
 #pragma unroll
     for (int j = K + 1; j < 4; ++j) gjs_fmac_bcast<C>(c[j], g);
-    if constexpr (K < 3) gjs_fmac_bcast<C>(bop, g);  // quarter q: column q of Aug
-    else bop = fma(gjs_bcast_c<C>(bop), g, bop);     // (the MFMA's B operand: a padded write)
+    // bop = Aug - S (quarter q: column q of Aug less the identity column e_{4 PN + q}), whose pivot-row
+    // entry is Aug's less 1 in quarter K: Aug += Aug[C] g is bop += bop[C] g + [q == K] g
+    const double dk = q == K ? 1.0 : 0.0;
+    if constexpr (K < 3) {
+        gjs_fmac_bcast<C>(bop, g);
+        bop = fma(dk, g, bop);
+    } else {
+        bop = fma(gjs_bcast_c<C>(bop) + dk, g, bop);  // (the MFMA's B operand: a padded write)
+    }
     myinv = i == C ? r : myinv;
     GJM_STAMP(8 * PN + 2 + K, c[K < 3 ? K + 1 : 3]);
 }
@@ -301,27 +309,34 @@ template <int PN>
 __device__ __forceinline__ void gjs_panel(gjm_d4& R, double (&c)[4], GjsOps<PN>& ops, double& myinv, double* sImg,
                                           int i, int q) {
     GJM_STAMP(8 * PN, c[0]);
-    double bop = i == 4 * PN + q ? 1.0 : 0.0;   // Aug's columns before the panel: the identity's
-    gjs_step<PN, 0>(c, bop, myinv, i);
-    gjs_step<PN, 1>(c, bop, myinv, i);
+    double bop = 0.0;   // Aug - S before the panel (Aug's columns: the identity's)
+    gjs_step<PN, 0>(c, bop, myinv, i, q);
+    gjs_step<PN, 1>(c, bop, myinv, i, q);
     if constexpr (PN > 0) {   // this panel's image (the previous MFMA's system), off the step chain
+        // (the write waits for that MFMA: kept after step 1, where it has long completed)
+        __builtin_amdgcn_sched_barrier(0);
         gjs_image(R, sImg, i, q);
         ops.read(sImg, i, q);
+        // (a scheduling barrier: the image and the operand reads stay here, their LDS latency under
+        // steps 2 and 3, instead of being sunk to the MFMAs on the chain)
+        __builtin_amdgcn_sched_barrier(0);
     }
-    gjs_step<PN, 2>(c, bop, myinv, i);
-    gjs_step<PN, 3>(c, bop, myinv, i);
+    gjs_step<PN, 2>(c, bop, myinv, i, q);
+    gjs_step<PN, 3>(c, bop, myinv, i, q);
     GJM_STAMP(8 * PN + 6, bop);
-    const bool prow = (i >> 2) == PN;   // the panel's pivot rows: zero in C (E J = (J - S S^T J) + Aug S^T J)
+    // E J = J + (Aug - S) S^T J: C is the system itself (no pivot-row zeroing)
     if constexpr (PN < 3) {   // the next panel's columns first: the step chain waits for them only
-        const gjm_d4 c2 = {prow ? 0.0 : ops.c2[0], prow ? 0.0 : ops.c2[1], prow ? 0.0 : ops.c2[2], prow ? 0.0 : ops.c2[3]};
+        const gjm_d4 c2 = {ops.c2[0], ops.c2[1], ops.c2[2], ops.c2[3]};
         const gjm_d4 nx = __builtin_amdgcn_mfma_f64_16x16x4f64(ops.a2op, bop, c2, 0, 0, 0);
         c[0] = nx[0];
         c[1] = nx[1];
         c[2] = nx[2];
         c[3] = nx[3];
     }
-    const gjm_d4 rz = {prow ? 0.0 : R[0], prow ? 0.0 : R[1], prow ? 0.0 : R[2], prow ? 0.0 : R[3]};
-    R = __builtin_amdgcn_mfma_f64_16x16x4f64(ops.aop, bop, rz, 0, 0, 0);
+    R = __builtin_amdgcn_mfma_f64_16x16x4f64(ops.aop, bop, R, 0, 0, 0);
+    // (both MFMAs issue here: the system's is not deferred past the next panel's steps, whose image
+    // write would then wait for it on the chain)
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 // Solve with the pivot order perm (perm[C] = the row that pivots column C).  Returns whether the
