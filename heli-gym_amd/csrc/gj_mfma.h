@@ -340,7 +340,8 @@ __device__ __forceinline__ void gjs_panel(gjm_d4& R, double (&c)[4], GjsOps<PN>&
 }
 
 // Solve with the pivot order perm (perm[C] = the row that pivots column C).  Returns whether the
-// solution passed the residual test (wave-uniform); x is in sX either way.
+// solution passed the residual test (wave-uniform; a pass implies every component is finite); x is in
+// sX either way.
 __device__ __forceinline__ bool gjs_solve(const double* sE, int es, double s, int src, const double* sYt,
                                           const int8_t* perm, double* sImg, double* sX, int l) {
     const int i = l & 15, q = l >> 4;
@@ -398,7 +399,10 @@ __device__ __forceinline__ bool gjs_solve(const double* sE, int es, double s, in
         mag0 = fma(fabs(j0[k]), fabs(x0[k]), mag0);
     }
     const double r = (gjs_quarter_sum(dot) + dot0) - b;
-    const bool good = fabs(r) <= kGjsTol * ((gjs_quarter_sum(mag) + mag0) + fabs(b));   // (false for a non-finite x)
+    const double scale = (gjs_quarter_sum(mag) + mag0) + fabs(b);
+    // (a non-finite x fails: a NaN compares false, and an infinite one makes the scale infinite; the
+    // lanes together hold every component, so the caller need not check x again)
+    const bool good = fabs(r) <= kGjsTol * scale && scale < INFINITY;
     GJM_STAMP(33, r);
     return __ballot(!good) == 0;
 }

@@ -670,7 +670,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
 #pragma unroll
                 for (int k = 0; k < 16; ++k) {
 #if HG_RT_XLDS
-                    fin = fin && isfinite(sX[k]);
+                    fin = fin && (solved || isfinite(sX[k]));   // (a passed residual test implies finite)
 #else
                     dir[k] = sX[k];
                     fin = fin && isfinite(dir[k]);
