@@ -1492,6 +1492,10 @@ struct hg_env {
     hg::TrimSetup setup;                    // trim condition -> Newton setup (host copy)
     hg::TrimSetup* setup_dev = nullptr;     // ... and device copy (re-trim kernel)
     Params<double>* pd_dev = nullptr;       // fp64 model constants for the re-trim kernel
+    // one allocation (trim_block) holds the re-trim job-count ring and counters, the trim setup and the
+    // fp64 constants: the step kernel's count atomics keep that page's translation warm, and a trim's
+    // first setup / constant loads no longer wait for a page walk (2 us of its start-up)
+    void* trim_block = nullptr;
     float* retrim_wind = nullptr;           // reset_mode RETRIM work buffers
     int32_t* retrim_list = nullptr;         // hg_reset's masked envs (their winds by env)
     int4* retrim_recs = nullptr;            // a step's auto-reset jobs {env, wind}
@@ -1856,8 +1860,8 @@ static void release(hg_env* e) {
         (void)hipModuleUnload(e->rtc_mod);
     }
     dfree(e->hmap); dfree(e->state); dfree(e->az); dfree(e->tmpl_dev); dfree(e->params_dev);
-    dfree(e->setup_dev); dfree(e->pd_dev); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_recs);
-    dfree(e->retrim_count); dfree(e->retrim_ring); dfree(e->ov_recs); dfree(e->ov_ring); dfree(e->fused_ring);
+    dfree(e->trim_block); dfree(e->retrim_wind); dfree(e->retrim_list); dfree(e->retrim_recs);
+    dfree(e->ov_recs); dfree(e->ov_ring); dfree(e->fused_ring);
     dfree(e->tmpl_env); dfree(e->setup_batch);
     delete e;
 }
@@ -1940,16 +1944,23 @@ int32_t hg_create(const hg_config* cfg, const double* terrain_ft, int32_t rows, 
     if ((err = hipMemset(e->tmpl_dev, 0, kTplAlloc)) != hipSuccess) return cleanup(err, "hipMemset template");
     if ((err = hipMemcpy(e->tmpl_dev, &e->tmpl, sizeof(e->tmpl), hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy template");
-    if ((err = hipMalloc(&e->setup_dev, sizeof(hg::TrimSetup))) != hipSuccess) return cleanup(err, "hipMalloc setup");
+    {   // [0, 64) the job-count ring, [64, 128) the counters, then the setup and the constants
+        constexpr size_t kSetupOff = 128;
+        constexpr size_t kPdOff = (kSetupOff + sizeof(hg::TrimSetup) + 255) / 256 * 256;
+        constexpr size_t kBlock = kPdOff + sizeof(Params<double>);
+        static_assert(kBlock <= 4096, "the trim block fits one page");
+        if ((err = hipMalloc(&e->trim_block, 4096)) != hipSuccess) return cleanup(err, "hipMalloc trim block");
+        if ((err = hipMemset(e->trim_block, 0, 4096)) != hipSuccess) return cleanup(err, "hipMemset trim block");
+        char* b = static_cast<char*>(e->trim_block);
+        e->retrim_ring = reinterpret_cast<int32_t*>(b);
+        e->retrim_count = reinterpret_cast<int32_t*>(b + 64);
+        e->setup_dev = reinterpret_cast<hg::TrimSetup*>(b + kSetupOff);
+        e->pd_dev = reinterpret_cast<Params<double>*>(b + kPdOff);
+    }
     if ((err = hipMemcpy(e->setup_dev, &e->setup, sizeof(e->setup), hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy setup");
-    if ((err = hipMalloc(&e->pd_dev, sizeof(Params<double>))) != hipSuccess) return cleanup(err, "hipMalloc params64");
     if ((err = hipMemcpy(e->pd_dev, &e->Pd, sizeof(e->Pd), hipMemcpyHostToDevice)) != hipSuccess)
         return cleanup(err, "hipMemcpy params64");
-    if ((err = hipMalloc(&e->retrim_count, 5 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim");
-    if ((err = hipMemset(e->retrim_count, 0, 5 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim");
-    if ((err = hipMalloc(&e->retrim_ring, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc retrim ring");
-    if ((err = hipMemset(e->retrim_ring, 0, 3 * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset retrim ring");
     if ((err = hipMalloc(&e->fused_ring, 3 * kFusedSlot * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMalloc fused ring");
     if ((err = hipMemset(e->fused_ring, 0, 3 * kFusedSlot * sizeof(int32_t))) != hipSuccess) return cleanup(err, "hipMemset fused ring");
     if (cfg->reset_mode == HG_RESET_RETRIM) {

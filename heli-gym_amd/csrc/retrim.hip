@@ -18,6 +18,17 @@
 #ifndef HG_RT_XLDS
 #define HG_RT_XLDS 0
 #endif
+// The Jacobian column re-materialised each Newton round (retrim_body.h HG_RT_OPAQUE_COL): here it
+// shortens the trim (same-step re-trim 28.96 -> 28.83 us), in the overlapped launch it costs 0.6 us
+// (scripts/gpu_r06_ab.sh), so only this translation unit sets it.
+#ifndef HG_RT_OPAQUE_COL
+#define HG_RT_OPAQUE_COL 1
+#endif
+// The first job's setup written to LDS at entry (retrim_body.h HG_RT_SETUP_LDS): same-step re-trim
+// 29.56 -> 28.85 us; the overlapped launch is 0.2 us slower with it and leaves it off.
+#ifndef HG_RT_SETUP_LDS
+#define HG_RT_SETUP_LDS 1
+#endif
 #include "retrim_body.h"
 
 namespace hgk {

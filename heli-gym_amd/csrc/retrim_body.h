@@ -409,7 +409,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     __shared__ double sE[42 * kEStride];   // rows 32..41: the line-search trials' evaluations
     __shared__ double sYt[16];       // the trim's target derivatives y* (its right-hand side is y(src) - y*)
     __shared__ double sX[16];        // the solution (Newton direction), by column
-    __shared__ double sXc[HG_RT_XLDS ? 16 : 1];   // HG_RT_XLDS: the current iterate
+    __shared__ double sXc[16];       // HG_RT_XLDS: the current iterate (else the first job's x0)
     __shared__ double sExt[7];       // observation terms of the current iterate
     __shared__ double sRow[HG_GJ_LDS ? 64 * kRowStride : 2];   // HG_GJ_LDS: the rows of the solve
     __shared__ double sImg[HG_GJ_MFMA ? 16 * kImgStride : 2];  // HG_GJ_MFMA: the system's image per panel
@@ -450,6 +450,26 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
     const int8_t piv_l = T0->piv[l >> 4][l & 15];
     constexpr int kPWords = (int)(sizeof(hg::Params<double>) / 4);
     const uint32_t pf = reinterpret_cast<const uint32_t*>(P_p)[min(16 * l, kPWords - 1)];
+#ifndef HG_RT_SETUP_LDS   // (retrim.hip sets it; the overlapped launch is 0.2 us faster without)
+#define HG_RT_SETUP_LDS 0
+#endif
+#if HG_GJ_MFMA && HG_GJ_STATIC && HG_RT_SETUP_LDS
+    // the first job's setup goes straight to LDS (the loop skips it for that job) and the prefetch is
+    // consumed here, all in one wait with the job count and record: held in registers into the Newton
+    // loop they were spilled to scratch, and each spill waited for its load in turn (2 us of the
+    // start-up, scripts/retrim_startup.py)
+    if (l < 16) {
+        sYt[l] = yt_l;
+        sXc[l] = x0_l;
+    }
+    sPiv[l] = piv_l;
+    const bool use_piv0 = __builtin_amdgcn_readfirstlane(piv_l) >= 0;   // (lane 0: piv[0][0])
+    asm volatile("" ::"v"(pf));
+    constexpr bool kSetupInLds = true;
+#else
+    constexpr bool kSetupInLds = false;
+    constexpr bool use_piv0 = false;   // (unused)
+#endif
 #if HG_RT_VLOAD
     const int4 rec0 = has_rec0 ? make_int4(__builtin_amdgcn_readfirstlane(rec0_v.x), __builtin_amdgcn_readfirstlane(rec0_v.y),
                                            __builtin_amdgcn_readfirstlane(rec0_v.z), __builtin_amdgcn_readfirstlane(rec0_v.w))
@@ -468,6 +488,12 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             g_rt_dbg[k][2] = a.ov + (a.list ? 2 : 0) + (a.recs ? 4 : 0);
             g_rt_dbg[k][3] = rec0.x;
         }
+    }
+#endif
+#if HG_TIMING
+    if (first == 0) {   // the job count and first record have arrived
+        asm volatile("" ::"s"((int)jobs), "s"(rec0.x));
+        if (l == 0) g_rt_timing[60] = __builtin_amdgcn_s_memtime();
     }
 #endif
     if (a.count && jobs > a.n) {   // a queue holds at most one job per env
@@ -537,11 +563,22 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
         const hg::TrimSetup& T = a.T[a.setup_stride ? job : 0];
         const bool j0 = job == first || !Tstride_p;   // (its setup requested at entry: every job's, with one setup)
 #if HG_GJ_MFMA && HG_GJ_STATIC
-        const int8_t piv_v = j0 ? piv_l : T.piv[l >> 4][l & 15];
-        sPiv[l] = piv_v;
-        const bool use_piv = __builtin_amdgcn_readfirstlane(piv_v) >= 0;   // (lane 0: piv[0][0])
+        bool use_piv;
+        if (kSetupInLds && j0) {   // (the entry's: this job's setup is the first job's)
+            use_piv = use_piv0;
+        } else {
+            const int8_t piv_v = j0 ? piv_l : T.piv[l >> 4][l & 15];
+            sPiv[l] = piv_v;
+            use_piv = __builtin_amdgcn_readfirstlane(piv_v) >= 0;   // (lane 0: piv[0][0])
+        }
 #endif
-        if (l < 16) sYt[l] = j0 ? yt_l : T.yt[l];   // (read after the first round's lds_order)
+        if (l < 16 && !(kSetupInLds && j0)) sYt[l] = j0 ? yt_l : T.yt[l];   // (read after the first round's lds_order)
+#if HG_TIMING
+        if (job == 0) {   // the setup has arrived
+            asm volatile("" ::"v"(yt_l), "v"(x0_l));
+            if (l == 0) g_rt_timing[59] = __builtin_amdgcn_s_memtime();
+        }
+#endif
         double W[3] = {P.wm[0], P.wm[1], P.wm[2]};   // NULL wind: the mean wind (helicopter.py:55)
         if (a.recs) {
             W[0] = (double)__int_as_float(rec.y);
@@ -562,12 +599,19 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
 #pragma unroll
         for (int k = 0; k < 16; ++k) ye[k] = 0.0;
 #if HG_RT_XLDS
-        if (l < 16) { sXc[l] = j0 ? x0_l : T.x0[l]; sX[l] = 0.0; }
+        if (l < 16) {
+            // (the iterate: only the first job's is the entry's, a later job starts from its setup again)
+            if (!(kSetupInLds && job == first)) sXc[l] = kSetupInLds ? T.x0[l] : (j0 ? x0_l : T.x0[l]);
+            sX[l] = 0.0;
+        }
         lds_order();
 #else
         double x[16], dir[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) { x[k] = j0 ? read_lane(x0_l, k) : T.x0[k]; dir[k] = 0.0; }
+        for (int k = 0; k < 16; ++k) {
+            x[k] = kSetupInLds ? (job == first ? sXc[k] : T.x0[k]) : (j0 ? read_lane(x0_l, k) : T.x0[k]);
+            dir[k] = 0.0;
+        }
 #endif
         double tol = 0;
         int it = 0, kind = kRoundFirst, src = 32, round = 0;
@@ -584,11 +628,19 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
             const double sl = l < 32 ? (kind == kRoundNormal ? 1.0 : 0.0)
                                      : ((kind == kRoundNormal && j < hg::kTrimLineSearch) ? ldexp(1.0, -j) : 0.0);
             const double pe = l < 16 ? eps : -eps;
+#ifndef HG_RT_OPAQUE_COL
+#define HG_RT_OPAQUE_COL 0
+#endif
+            // (HG_RT_OPAQUE_COL: the column re-materialised each round; hoisted out of the Newton loop,
+            // the 16 selects' masks and addends take 32 VGPRs and push the loop's scalars into a long
+            // spill prologue)
+            int cr = c;
+            if (HG_RT_OPAQUE_COL) asm volatile("" : "+v"(cr));
             double xe[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const double b = fma(-sl, HG_DIR(k), HG_X(k));
-                xe[k] = (l < 32 && c == k) ? b + pe : b;
+                xe[k] = (l < 32 && cr == k) ? b + pe : b;
             }
             RSTAMP(1 + 4 * round, "v"(xe[0]));
             if (kind != kRoundJacobian || l < 32) {
@@ -775,7 +827,7 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
         FSTAMP(2);
         lds_order();   // the next job's writes come after this job's reads
     }
-    if (pf == 0x7FC00001u && jobs == -12345 && a.bad_jobs) atomicAdd(a.bad_jobs, 0);   // (keeps the prefetch)
+    if (!kSetupInLds && pf == 0x7FC00001u && jobs == -12345 && a.bad_jobs) atomicAdd(a.bad_jobs, 0);   // (keeps the prefetch)
 }
 
 }  // namespace
