@@ -1492,9 +1492,9 @@ struct hg_env {
     hg::TrimSetup setup;                    // trim condition -> Newton setup (host copy)
     hg::TrimSetup* setup_dev = nullptr;     // ... and device copy (re-trim kernel)
     Params<double>* pd_dev = nullptr;       // fp64 model constants for the re-trim kernel
-    // one allocation (trim_block) holds the re-trim job-count ring and counters, the trim setup and the
-    // fp64 constants: the step kernel's count atomics keep that page's translation warm, and a trim's
-    // first setup / constant loads no longer wait for a page walk (2 us of its start-up)
+    // one allocation (trim_block, one page) holds the re-trim job-count ring and counters, the trim
+    // setup and the fp64 constants (placed there to keep the trims' first loads on a page the step
+    // kernel's count atomics touch; no measurable change in the start-up, scripts/retrim_startup.py)
     void* trim_block = nullptr;
     float* retrim_wind = nullptr;           // reset_mode RETRIM work buffers
     int32_t* retrim_list = nullptr;         // hg_reset's masked envs (their winds by env)
