@@ -339,6 +339,97 @@ __device__ __forceinline__ void gjs_panel(gjm_d4& R, double (&c)[4], GjsOps<PN>&
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// GJS_BLOCK_INV: the panel's four pivot steps replaced by the inverse of its 4 x 4 pivot block D (rows
+// 4 PN .. 4 PN + 3 of the panel's columns, broadcast to every lane).  Quarter q solves D y = e_q by
+// elimination in the given order (the pivots are the four steps' own), so the lanes of quarter q hold
+// column q of D^-1, and the panel's transformation is E = I + A S^T with A = (S - M) D^-1 (M: the
+// panel's columns; the pivot rows come out scaled to the identity, so x needs no division at the
+// end).  Four dependent reciprocals and the eliminations between them instead of four steps with a
+// broadcast, a reciprocal and an update chain each.
+#ifndef GJS_BLOCK_INV
+#define GJS_BLOCK_INV 1
+#endif
+__device__ __forceinline__ double gjs_rcp1(double p) {   // v_rcp_f64 and one Newton step
+    const double r = __builtin_amdgcn_rcp(p);
+    return fma(r, fma(-p, r, 1.0), r);
+}
+template <int PN>
+__device__ __forceinline__ void gjs_panel_blk(gjm_d4& R, double (&c)[4], GjsOps<PN>& ops, double* sImg, int i, int q) {
+    constexpr int C0 = 4 * PN;
+    GJM_STAMP(8 * PN, c[0]);
+    double d[4][4];   // D[k][v] = c[v] of lane C0 + k (every quarter holds the same rows)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        d[0][v] = gjs_bcast_c<C0>(c[v]);
+        d[1][v] = gjs_bcast_c<C0 + 1>(c[v]);
+        d[2][v] = gjs_bcast_c<C0 + 2>(c[v]);
+        d[3][v] = gjs_bcast_c<C0 + 3>(c[v]);
+    }
+    double e0 = q == 0 ? 1.0 : 0.0, e1 = q == 1 ? 1.0 : 0.0, e2 = q == 2 ? 1.0 : 0.0, e3 = q == 3 ? 1.0 : 0.0;
+    double w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = (i == C0 + k ? 1.0 : 0.0) - c[k];
+    // elimination in the given order (the pivots are D's leading diagonal as it is reduced)
+    const double r0 = gjs_rcp1(d[0][0]);
+    {
+        const double l1 = d[1][0] * r0, l2 = d[2][0] * r0, l3 = d[3][0] * r0;
+#pragma unroll
+        for (int v = 1; v < 4; ++v) {
+            d[1][v] = fma(-l1, d[0][v], d[1][v]);
+            d[2][v] = fma(-l2, d[0][v], d[2][v]);
+            d[3][v] = fma(-l3, d[0][v], d[3][v]);
+        }
+        e1 = fma(-l1, e0, e1);
+        e2 = fma(-l2, e0, e2);
+        e3 = fma(-l3, e0, e3);
+    }
+    GJM_STAMP(8 * PN + 2, d[1][1]);
+    if constexpr (PN > 0) {   // this panel's image (the previous MFMA's system), off the chain
+        __builtin_amdgcn_sched_barrier(0);
+        gjs_image(R, sImg, i, q);
+        ops.read(sImg, i, q);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    const double r1 = gjs_rcp1(d[1][1]);
+    {
+        const double l2 = d[2][1] * r1, l3 = d[3][1] * r1;
+#pragma unroll
+        for (int v = 2; v < 4; ++v) {
+            d[2][v] = fma(-l2, d[1][v], d[2][v]);
+            d[3][v] = fma(-l3, d[1][v], d[3][v]);
+        }
+        e2 = fma(-l2, e1, e2);
+        e3 = fma(-l3, e1, e3);
+    }
+    GJM_STAMP(8 * PN + 3, d[2][2]);
+    const double r2 = gjs_rcp1(d[2][2]);
+    {
+        const double l3 = d[3][2] * r2;
+        d[3][3] = fma(-l3, d[2][3], d[3][3]);
+        e3 = fma(-l3, e2, e3);
+    }
+    const double r3 = gjs_rcp1(d[3][3]);
+    // back substitution: y = column q of D^-1
+    const double y3 = e3 * r3;
+    const double y2 = fma(-d[2][3], y3, e2) * r2;
+    const double y1 = fma(-d[1][2], y2, fma(-d[1][3], y3, e1)) * r1;
+    const double y0 = fma(-d[0][1], y1, fma(-d[0][2], y2, fma(-d[0][3], y3, e0))) * r0;
+    GJM_STAMP(8 * PN + 4, y0);
+    // bop = A[i][q] = sum_k W[i][k] y_k with W = S - M (formed off the chain, as soon as c is)
+    const double bop = fma(w[0], y0, fma(w[1], y1, fma(w[2], y2, w[3] * y3)));
+    GJM_STAMP(8 * PN + 6, bop);
+    if constexpr (PN < 3) {   // the next panel's columns first: the chain waits for them only
+        const gjm_d4 c2 = {ops.c2[0], ops.c2[1], ops.c2[2], ops.c2[3]};
+        const gjm_d4 nx = __builtin_amdgcn_mfma_f64_16x16x4f64(ops.a2op, bop, c2, 0, 0, 0);
+        c[0] = nx[0];
+        c[1] = nx[1];
+        c[2] = nx[2];
+        c[3] = nx[3];
+    }
+    R = __builtin_amdgcn_mfma_f64_16x16x4f64(ops.aop, bop, R, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 // Solve with the pivot order perm (perm[C] = the row that pivots column C).  Returns whether the
 // solution passed the residual test (wave-uniform; a pass implies every component is finite); x is in
 // sX either way.
@@ -372,6 +463,14 @@ __device__ __forceinline__ bool gjs_solve(const double* sE, int es, double s, in
     GjsOps<1> o1;
     GjsOps<2> o2;
     GjsOps<3> o3;
+#if GJS_BLOCK_INV
+    gjs_panel_blk<0>(R, c, o0, sImg, i, q);
+    gjs_panel_blk<1>(R, c, o1, sImg, i, q);
+    gjs_panel_blk<2>(R, c, o2, sImg, i, q);
+    gjs_panel_blk<3>(R, c, o3, sImg, i, q);
+    GJM_STAMP(32, R[0]);
+    if (l < 16) sX[i] = R[0];   // (the pivot rows scaled to the identity)
+#else
     double myinv = 0.0;
     gjs_panel<0>(R, c, o0, myinv, sImg, i, q);
     gjs_panel<1>(R, c, o1, myinv, sImg, i, q);
@@ -379,6 +478,7 @@ __device__ __forceinline__ bool gjs_solve(const double* sE, int es, double s, in
     gjs_panel<3>(R, c, o3, myinv, sImg, i, q);
     GJM_STAMP(32, R[0]);
     if (l < 16) sX[i] = R[0] * myinv;
+#endif
     // the residual of the permuted system: J x - b from the system as given
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "heli-gym_amd")]
 SO = os.path.join(ROOT, "build", "gj_solve.so")
 # (name, extra flags): the stamped build, the same without stamps (true cycles), one Newton step after v_rcp_f64
-VARIANTS = [("gj_solve", []), ("gj_solve_nostamp", ["-DGJ_NO_STAMPS"]), ("gj_solve_nr1", ["-DGJ_NO_STAMPS", "-DGJM_RCP_NR=1"])]
+VARIANTS = [("gj_solve", []), ("gj_solve_nostamp", ["-DGJ_NO_STAMPS"]), ("gj_solve_nr1", ["-DGJ_NO_STAMPS", "-DGJM_RCP_NR=1"]),
+            ("gj_solve_steps", ["-DGJ_NO_STAMPS", "-DGJS_BLOCK_INV=0"])]   # (the static solve's pivot steps)
 
 
 def build():
