@@ -663,8 +663,8 @@ __device__ __forceinline__ void step_body(float* __restrict__ state_p, int64_t n
     // a reset whose trim runs concurrently with this step -- a next-step reset in ov mode, any reset in
     // a fused launch: only the step counter is stored here, the trim writes the rest
 #ifndef HG_FUSED_NOTRIM   // diagnostic: 1, a fused launch's trim blocks leave at once and its resets
-#define HG_FUSED_NOTRIM 0   // take the template (the step's own cost in that launch); 2, the trim waves
-#endif                      // wait for their records but trim nothing
+#define HG_FUSED_NOTRIM 0   // take the template (the step's own cost in that launch)
+#endif
     const bool defer = FEAT && (a.ov_active || (a.fused_ctr && !HG_FUSED_NOTRIM)) && do_reset;
     defer_st = defer;
     if (active) {
@@ -945,7 +945,7 @@ __global__ __launch_bounds__(kStepBlock) __attribute__((amdgpu_waves_per_eu(2)))
     int64_t envoff_p, ParamArg Pa, const Template<float>* __restrict__ Tp, const StepArgs a, const hgk::RetrimArgs r,
     int32_t tb) {
     if ((int32_t)blockIdx.x < tb) {
-        if (HG_FUSED_NOTRIM != 1 && (kStepBlock == 64 || threadIdx.x < 64))
+        if (!HG_FUSED_NOTRIM && (kStepBlock == 64 || threadIdx.x < 64))
             hgk::retrim_jobs<true>(r, blockIdx.x, tb, rcount, rrecs, rT, rP, 0);
         return;
     }

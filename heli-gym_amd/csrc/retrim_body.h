@@ -546,9 +546,6 @@ __device__ __forceinline__ void retrim_jobs(const RetrimArgs& a, int64_t first, 
                             __builtin_amdgcn_readfirstlane(__hip_atomic_load(rp + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
                             __builtin_amdgcn_readfirstlane(__hip_atomic_load(rp + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
             if (l == 0) rp[0] = -1;   // the slot free for the next launch's queue
-#if defined(HG_FUSED_NOTRIM) && HG_FUSED_NOTRIM == 2
-            continue;
-#endif
         } else {
             rec = a.recs ? (job == first ? rec0 : a.recs[job]) : make_int4(0, 0, 0, 0);
             // every consumed record goes back to env -1, so that a fused launch (which waits for env >= 0)
