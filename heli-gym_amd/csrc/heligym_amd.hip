@@ -1719,8 +1719,11 @@ static hipError_t dispatch_task(const hg_env* e, hipStream_t s, const StepArgs& 
 
 // ov mode's launch: `ov_trim_blocks` trim blocks (the previous step's ends; blocks without a job exit at
 // once) ahead of the step's blocks -- never more than one per env (a step ends at most n episodes)
+#ifndef HG_OV_TB_DIV   // (A/B knob: the overlapped launch's trim blocks, n / 256 / this)
+#define HG_OV_TB_DIV 1
+#endif
 static inline int32_t ov_trim_blocks(int64_t n) {
-    int64_t b = n / 256;
+    int64_t b = n / 256 / HG_OV_TB_DIV;
     b = b < 64 ? 64 : (b > 1024 ? 1024 : b);
     return (int32_t)(b < n ? b : n);
 }

@@ -34,11 +34,10 @@
 namespace hgk {
 namespace {
 
-// one wave per SIMD: this kernel runs alone (a trim per wave, one wave per block), so the register
-// budget of a single wave is free -- its spills stay in registers (same-step re-trim 28.32 -> 28.07 us,
-// interleaved A/B, scripts/gpu_r06_ab.sh); the overlapped launch keeps two per SIMD for its step waves
+// (one wave per SIMD, the whole register budget of a single wave, measured in round 6: 28.07 against
+// 28.32 us per same-step re-trim step on one box, 28.28 against 28.27 on another; not adopted)
 #ifndef HG_RETRIM_WAVES
-#define HG_RETRIM_WAVES 1
+#define HG_RETRIM_WAVES 2
 #endif
 // count_p / recs_p / T_p / P_p / Tstride_p = a.count / a.recs / a.T / a.P / a.setup_stride: leading
 // arguments, preloaded into SGPRs (__graft_entry__.py builds this translation unit with
